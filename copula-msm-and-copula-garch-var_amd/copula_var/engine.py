@@ -1,0 +1,207 @@
+"""Host-side handle on the HIP quadrature engine (libcvq.so).
+
+``QuadraturePlan`` is the device replacement for the reference's quadrature
+stack: ``compute_integral`` replaces ValueAtRiskCalcualtion.compute_integral
+(utils/calc_var_class.py:179-212 -> utils/calc_integral/calc_integral.py:8-225)
+and ``calc_var`` replaces calc_var + bisection_algorithm
+(utils/calc_var_class.py:95-177, 250-309) with one device solve.
+The forecast-stage functions replace the per-date filters
+(msm_estimation.py:140-202, garch_estimation.py:190-231,
+mean_reverting_estimation.py:192-232).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+DEFAULT_SOLVE = dict(obj_var=0.05, first_guess=-3.0, second_guess=(-3.5, -2.0), min_var=-7.5,
+                     max_var=0.0, lower=-100.0, tolerance=1e-6)
+
+
+def solve_args(ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_guess=(-3.5, -2.0),
+               min_var=-7.5, max_var=0.0, lower=-100.0, tolerance=1e-6) -> N.CvqSolveArgs:
+    """calc_var arguments (calc_var_class.py:95) + its constants (:111-114, :257)."""
+    return N.CvqSolveArgs(float(obj_var), float(first_guess), float(second_guess[0]), float(second_guess[1]),
+                          float(min_var), float(max_var), float(lower), float(tolerance), float(ptf_mean))
+
+
+class QuadraturePlan:
+    """One device plan: static grid tables + copula + per-date inputs on one GPU."""
+
+    def __init__(self, model: str, copula: str, dim: int, x_values, step, densities, combos, weights,
+                 copula_params, vol_states=None, v_cap: float = 0.0, device: int = 0,
+                 strategy: str = "prefix"):
+        N.require_gpu()
+        self.model, self.copula, self.dim = model, copula, int(dim)
+        self.device = int(device)
+        self._x = N.f64(x_values)
+        self._step = N.f64(step)
+        self._dens = N.f64(densities)
+        self._combos = np.ascontiguousarray(np.asarray(combos).astype(np.int32))
+        self._w = N.f64(weights)
+        self._cp = N.f64(np.atleast_1d(np.asarray(copula_params, dtype=np.float64)))
+        self._vs = N.f64(vol_states) if vol_states is not None else None
+        q = self._dens.shape[1]
+        st = N.CvqStatic()
+        st.model = N.MODEL_KIND[model]
+        st.copula = N.COPULA_KIND[copula]
+        st.dim = self.dim
+        st.n = self._x.size
+        st.q = q
+        st.n_combos = self._combos.shape[0]
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        st.x_values, st.step, st.densities = dp(self._x), dp(self._step), dp(self._dens)
+        st.combos = self._combos.ctypes.data_as(C.POINTER(C.c_int32))
+        st.weights = dp(self._w)
+        st.vol_states = dp(self._vs) if self._vs is not None else None
+        st.copula_params = dp(self._cp)
+        st.n_copula_params = self._cp.size
+        st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT}[strategy]
+        st.v_cap = float(v_cap)
+        self._static = st
+        h = C.c_void_p()
+        N.check(N.lib().cvq_plan_create(C.byref(st), self.device, C.byref(h)), "cvq_plan_create")
+        self._h = h
+        self.T = 0
+        reach, rows = C.c_int64(), C.c_int32()
+        N.check(N.lib().cvq_plan_info(self._h, C.byref(reach), C.byref(rows)), "cvq_plan_info")
+        self.reach_nodes, self.rows = int(reach.value), int(rows.value)
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.lib().cvq_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        N.check(N.lib().cvq_plan_set_stream(self._h, C.c_void_p(stream_handle or 0)), "cvq_plan_set_stream")
+
+    # ------------------------------------------------------------ per-date inputs
+    def set_dates(self, integrations_params_t) -> None:
+        """integrations_params_t as the reference builds it: MSM (forecasts_by_states
+        (T,dim,q), forecasts (T,Q)); GARCH/UKF [sigma (T,dim)] (garch_estimation.py:231)."""
+        if self.model == "msm":
+            fbs, pi = integrations_params_t
+            a, b = N.f64(fbs), N.f64(pi)
+            T = a.shape[0]
+            N.check(N.lib().cvq_set_dates(self._h, T, N.ptr(a), N.ptr(b), N.MEM_HOST), "cvq_set_dates")
+        else:
+            sig = integrations_params_t[0] if isinstance(integrations_params_t, (list, tuple)) else integrations_params_t
+            a = N.f64(sig)
+            T = a.shape[0]
+            N.check(N.lib().cvq_set_dates(self._h, T, N.ptr(a), None, N.MEM_HOST), "cvq_set_dates")
+        self.T = int(T)
+
+    def set_dates_device(self, T: int, a_ptr: int, b_ptr: Optional[int] = None) -> None:
+        """Per-date inputs already resident in device memory (e.g. torch tensors' data_ptr())."""
+        N.check(N.lib().cvq_set_dates(self._h, int(T), C.c_void_p(a_ptr), C.c_void_p(b_ptr or 0), N.MEM_DEVICE),
+                "cvq_set_dates")
+        self.T = int(T)
+
+    # ------------------------------------------------------------ quadrature
+    def compute_integral(self, bounds) -> np.ndarray:
+        """Drop-in for ValueAtRiskCalcualtion.compute_integral(bounds) -> (T,)."""
+        b = N.f64(bounds)
+        if b.shape != (self.T, 2):
+            raise ValueError(f"bounds must have shape ({self.T}, 2)")
+        out = np.empty(self.T)
+        N.check(N.lib().cvq_slab(self._h, N.ptr(b), N.ptr(out), N.MEM_HOST), "cvq_slab")
+        return out
+
+    def calc_var(self, ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_guess=(-3.5, -2.0),
+                 **consts) -> Tuple[np.ndarray, int]:
+        """Drop-in for calc_var (calc_var_class.py:95-177): returns (VaR (T,), iterations)."""
+        args = solve_args(ptf_mean, obj_var, first_guess, second_guess, **consts)
+        out = np.empty(self.T)
+        it = C.c_int32(0)
+        N.check(N.lib().cvq_solve(self._h, C.byref(args), N.ptr(out), C.byref(it), N.MEM_HOST), "cvq_solve")
+        return out, int(it.value)
+
+    # ------------------------------------------------------------ device-resident solve
+    def solve_device(self, args: N.CvqSolveArgs, var_ptr: int) -> None:
+        """calc_var into a device buffer, in stream order, no host synchronisation."""
+        N.check(N.lib().cvq_solve(self._h, C.byref(args), C.c_void_p(var_ptr), None, N.MEM_DEVICE), "cvq_solve")
+
+    @staticmethod
+    def snap_stride(args: N.CvqSolveArgs) -> int:
+        s = C.c_int32()
+        N.check(N.lib().cvq_snap_stride(C.byref(args), C.byref(s)), "cvq_snap_stride")
+        return int(s.value)
+
+    def solve_local(self, args: N.CvqSolveArgs, header_ptr: int, snaps_ptr: int) -> None:
+        N.check(N.lib().cvq_solve_local(self._h, C.byref(args), C.c_void_p(header_ptr), C.c_void_p(snaps_ptr)),
+                "cvq_solve_local")
+
+    def solve_finalize(self, args: N.CvqSolveArgs, headers_ptr: int, n_ranks: int, snaps_ptr: int,
+                       dates_per_rank: int, T_total: int, var_ptr: int) -> None:
+        N.check(N.lib().cvq_solve_finalize(self._h, C.byref(args), C.c_void_p(headers_ptr), int(n_ranks),
+                                           C.c_void_p(snaps_ptr), int(dates_per_rank), int(T_total),
+                                           C.c_void_p(var_ptr)), "cvq_solve_finalize")
+
+
+# ====================================================================== forecasts
+def msm_filter(returns_c, n_in: int, k: int, m0: float, sig: float, b: float, gamma: float,
+               device: int = 0) -> np.ndarray:
+    """Filtered state probabilities at each window end, (T, 2**k).  returns_c: centred
+    returns of one asset, length n_in + T - 1 (windows returns_c[t:t+n_in])."""
+    r = N.f64(returns_c)
+    T = r.size - n_in + 1
+    out = np.empty((T, 1 << k))
+    N.check(N.lib().cvq_msm_filter(device, k, m0, sig, b, gamma, N.ptr(r), n_in, T, N.ptr(out), N.MEM_HOST),
+            "cvq_msm_filter")
+    return out
+
+
+def garch_forecast(returns_c, n_in: int, omega: float, alpha: float, beta: float, device: int = 0) -> np.ndarray:
+    r = N.f64(returns_c)
+    T = r.size - n_in + 1
+    out = np.empty(T)
+    N.check(N.lib().cvq_garch_forecast(device, omega, alpha, beta, N.ptr(r), n_in, T, N.ptr(out), N.MEM_HOST),
+            "cvq_garch_forecast")
+    return out
+
+
+def ukf_forecast(returns_c, n_in: int, a: float, l: float, q: float, device: int = 0) -> np.ndarray:
+    r = N.f64(returns_c)
+    T = r.size - n_in + 1
+    out = np.empty(T)
+    N.check(N.lib().cvq_ukf_forecast(device, a, l, q, N.ptr(r), n_in, T, N.ptr(out), N.MEM_HOST),
+            "cvq_ukf_forecast")
+    return out
+
+
+def msm_loglik(returns, k: int, params, device: int = 0) -> np.ndarray:
+    """params (B, 4) rows (m0, sigma, b, gamma) -> (B,) log-likelihoods."""
+    r, p = N.f64(returns), N.f64(np.atleast_2d(params))
+    out = np.empty(p.shape[0])
+    N.check(N.lib().cvq_msm_loglik(device, k, N.ptr(p), p.shape[0], N.ptr(r), r.size, N.ptr(out), N.MEM_HOST),
+            "cvq_msm_loglik")
+    return out
+
+
+def garch_loglik(returns, params, device: int = 0) -> np.ndarray:
+    """params (B, 3) rows (omega, alpha, beta)."""
+    r, p = N.f64(returns), N.f64(np.atleast_2d(params))
+    out = np.empty(p.shape[0])
+    N.check(N.lib().cvq_garch_loglik(device, N.ptr(p), p.shape[0], N.ptr(r), r.size, N.ptr(out), N.MEM_HOST),
+            "cvq_garch_loglik")
+    return out
+
+
+def ukf_loglik(returns, params, device: int = 0) -> np.ndarray:
+    """params (B, 3) rows (a, l, q)."""
+    r, p = N.f64(returns), N.f64(np.atleast_2d(params))
+    out = np.empty(p.shape[0])
+    N.check(N.lib().cvq_ukf_loglik(device, N.ptr(p), p.shape[0], N.ptr(r), r.size, N.ptr(out), N.MEM_HOST),
+            "cvq_ukf_loglik")
+    return out

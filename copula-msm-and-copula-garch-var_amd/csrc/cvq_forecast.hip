@@ -1,0 +1,528 @@
+// cvq_forecast.hip -- per-date forecast stage + batched in-sample likelihoods (gfx950).
+//
+// Reference:
+//   MSM   markov_switching_multifractal/calc_prob.py:8-142, calc_marginals.py:33-38,
+//         utils/model_estimation/model/msm_estimation.py:140-202
+//   GARCH garch/estimation.py:40-125, garch/forecast.py:5-19
+//   UKF   kalman_mean_reverting/estimate.py:53-281, forecast.py:5-12
+//
+// Each rolling window restarts its filter (load_data.py:130-137), so windows are
+// independent: the batch axis is (window) for forecasts and (parameter candidate)
+// for likelihoods.  The MSM transition matrix is a Kronecker product of k 2x2
+// blocks (calc_prob.py:91-101), so A.pi is applied as k butterflies instead of an
+// S x S mat-vec: a quad of lanes holds one window's 2^k states, low state bits
+// in registers, the top two bits across the quad (__shfl_xor 1, 2).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "cvq_common.h"
+
+using namespace cvq;
+
+namespace {
+
+constexpr double kInvSqrt2Pi = 0.3989422804014327;
+
+struct MsmParams {
+    double p[8];       // stay probabilities p_c = 1 - gamma_c / 2 (calc_prob.py:93-95)
+    double qv[8];      // 1 - p_c
+    double vs[128];    // vol states sqrt(prod M_s) * sigma (calc_prob.py:103-108)
+};
+
+MsmParams msm_params(int k, double m0, double sigma, double b, double gamma) {
+    MsmParams P{};
+    for (int c = 0; c < k; ++c) {
+        const double gk = 1 - std::pow(1 - gamma, std::pow(b, (double)c));
+        P.p[c] = 1 - gk / 2;
+        P.qv[c] = 1 - P.p[c];
+    }
+    const int S = 1 << k;
+    for (int s = 0; s < S; ++s) {
+        double prod = 1.0;
+        for (int c = 0; c < k; ++c) {            // itertools.product order: component c <-> bit k-1-c
+            const int bit = (s >> (k - 1 - c)) & 1;
+            prod = (c == 0) ? (bit ? 2 - m0 : m0) : prod * (bit ? 2 - m0 : m0);
+        }
+        P.vs[s] = std::sqrt(prod) * sigma;
+    }
+    return P;
+}
+
+__device__ __forceinline__ double cond_prob(double r, double vs) {
+    const double z = r / vs;
+    return (1 / (vs * 2.5066282746310002)) * exp(-0.5 * (z * z));   // calc_prob.py:116-117
+}
+
+template <int K>
+struct Quad {
+    static constexpr int S = 1 << K;
+    static constexpr int L = S < 4 ? S : 4;        // lanes per window
+    static constexpr int SL = S / L;               // states per lane
+    static constexpr int LB = (SL == 1) ? 0 : __builtin_ctz(SL);
+};
+
+// One Hamilton-filter step (calc_bayes_upd_numba, calc_prob.py:51-69) for a
+// quad-resident state vector.  v: this lane's SL states (state s = lane_q*SL + j),
+// cv: the matching conditional densities.  Returns the normaliser.
+template <int K>
+__device__ __forceinline__ double msm_step(double (&v)[Quad<K>::SL], const double (&cv)[Quad<K>::SL],
+                                           const MsmParams& P, bool* zero) {
+    constexpr int SL = Quad<K>::SL, L = Quad<K>::L, LB = Quad<K>::LB;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const int pos = K - 1 - c;                 // component c <-> state bit k-1-c
+        const double pc = P.p[c], qc = P.qv[c];
+        if (pos < LB) {
+            double nv[SL];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) nv[j] = pc * v[j] + qc * v[j ^ (1 << pos)];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) v[j] = nv[j];
+        } else {
+            const int m = 1 << (pos - LB);
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                const double o = __shfl_xor(v[j], m, 64);
+                v[j] = pc * v[j] + qc * o;
+            }
+        }
+    }
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+        v[j] = v[j] * cv[j];
+        part += v[j];
+    }
+    double tot = part;
+    if (L >= 2) tot += __shfl_xor(tot, 1, 64);
+    if (L >= 4) tot += __shfl_xor(tot, 2, 64);
+    *zero = !(tot != 0.0);
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = v[j] / tot;
+    return tot;
+}
+
+// cond[i][s] for every return of the series (shared by all windows containing i).
+__global__ void k_msm_cond(MsmParams P, int S, const double* __restrict__ r, long long N, double* __restrict__ cond) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * S) return;
+    cond[idx] = cond_prob(r[idx / S], P.vs[idx % S]);
+}
+
+// Filtered state probabilities at the end of each window (calc_forecasts).
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_filter(MsmParams P, const double* __restrict__ cond, long long n_in,
+                                                    long long T, double* __restrict__ out, int* err) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long t = gid / L;
+    const int lane_q = (int)(gid % L);
+    const bool active = t < T;
+    const long long tt = active ? t : T - 1;
+    double v[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = 1.0 / S;               // equi_prob (calc_prob.py:12-13)
+    bool bad = false;
+    for (long long i = 0; i < n_in; ++i) {
+        double cv[SL];
+        const double* row = cond + (tt + i) * S + lane_q * SL;
+#pragma unroll
+        for (int j = 0; j < SL; ++j) cv[j] = row[j];
+        bool z;
+        msm_step<K>(v, cv, P, &z);
+        bad |= z;
+    }
+    if (!active) return;
+    if (bad) atomicOr(err, 1);
+#pragma unroll
+    for (int j = 0; j < SL; ++j) out[t * S + lane_q * SL + j] = v[j];
+}
+
+// Batched MSM log-likelihood (calc_prob.py:134-142 -> :36-47): one quad per candidate.
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_loglik(const MsmParams* __restrict__ Ps, long long B,
+                                                    const double* __restrict__ r, long long N, double* __restrict__ out) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long bi = gid / L;
+    const int lane_q = (int)(gid % L);
+    const bool active = bi < B;
+    const MsmParams& P = Ps[active ? bi : B - 1];
+    double v[SL], vs[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) { v[j] = 1.0 / S; vs[j] = P.vs[lane_q * SL + j]; }
+    double LL = 0.0;
+    bool dead = false;
+    for (long long i = 0; i < N; ++i) {
+        double cv[SL];
+        const double ri = r[i];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) cv[j] = cond_prob(ri, vs[j]);
+        bool z;
+        const double tot = msm_step<K>(v, cv, P, &z);
+        if (i >= 1) {
+            if (!(tot > 0.0)) dead = true; else LL += log(tot);
+        }
+        if (z) dead = true;
+    }
+    if (active && lane_q == 0) out[bi] = dead ? -__builtin_huge_val() : LL;
+}
+
+// ----------------------------------------------------------------- GARCH(1,1)
+__global__ void k_garch_forecast(double omega, double alpha, double beta, const double* __restrict__ r,
+                                 long long n_in, long long T, double* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const double* w = r + t;
+    double s2 = omega / (1 - alpha - beta);                     // estimation.py:52
+    for (long long i = 1; i < n_in; ++i) {
+        double v = omega + alpha * (w[i - 1] * w[i - 1]);
+        v = v + beta * s2;
+        s2 = (1e-7 > v) ? 1e-7 : v;                             // max(sigma2, epsilon)
+    }
+    const double rl = w[n_in - 1];
+    out[t] = sqrt(omega + alpha * (rl * rl) + beta * s2);      // forecast.py:14-19
+}
+
+__global__ void k_garch_loglik(const double* __restrict__ prm, long long B, const double* __restrict__ r, long long N,
+                               double* __restrict__ out) {
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double omega = prm[3 * b], alpha = prm[3 * b + 1], beta = prm[3 * b + 2];
+    double s2 = omega / (1 - alpha - beta);
+    double acc = 0.0;
+    for (long long i = 1; i < N; ++i) {
+        double v = omega + alpha * (r[i - 1] * r[i - 1]);
+        v = v + beta * s2;
+        s2 = (1e-7 > v) ? 1e-7 : v;
+        acc += log(2 * M_PI * s2) + (r[i] * r[i]) / s2;          // estimation.py:118-123
+    }
+    out[b] = -0.5 * acc;
+}
+
+// ----------------------------------------------------------------------- UKF
+struct UkfConst {
+    double wm0, wm1, wc0, wc1, wm2_0, wm2_1, phi;
+};
+
+UkfConst ukf_const(double alpha = 1.6, double beta = 2.0, double kappa = 1.75) {
+    const int L = 2;
+    const double lam = (alpha * alpha) * (L + kappa) - L;        // estimate.py:234
+    UkfConst c;
+    c.wm1 = 1 / (2 * (L + lam));
+    c.wm0 = lam / (L + lam);
+    c.wc1 = c.wm1;
+    c.wc0 = c.wm0 + (1 - alpha * alpha + beta);                  // :103-109
+    c.wm2_0 = lam / (L + lam);
+    c.wm2_1 = 1 / (2 * (L + lam));                               // :112-116
+    c.phi = std::sqrt(L + lam);
+    return c;
+}
+
+// Runs one UKF pass; returns false on the Z < 1e-10 failure (estimate.py:219-220).
+__device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const double* w, long long N,
+                         double* xmean_last, double* LL) {
+    double x = l, var = q;                                        // forecast.py:9: init (l, q)
+    double xm = 0.0, ll = 0.0;
+    for (long long t = 0; t < N; ++t) {
+        const double dvar = (var <= 0) ? var + 1e-8 : var;        // custom_cholesky :72-74
+        const double c0 = sqrt(dvar);
+        const double X1a[5] = {x, x + C.phi * c0, x + C.phi * 0.0, x - C.phi * c0, x - C.phi * 0.0};
+        const double X1b[5] = {0.0, 0.0 + C.phi * 0.0, 0.0 + C.phi * 1.0, 0.0 - C.phi * 0.0, 0.0 - C.phi * 1.0};
+        double X[5];
+        for (int i = 0; i < 5; ++i) X[i] = a * (X1a[i] - l) + l + q * X1b[i];   // f_vectorized :141
+        xm = X[0] * C.wm0;
+        for (int i = 1; i < 5; ++i) xm += X[i] * C.wm1;
+        double P = 0.0;
+        for (int i = 0; i < 5; ++i) {
+            const double d = X[i] - xm;
+            P += (d * (i == 0 ? C.wc0 : C.wc1)) * d;
+        }
+        const double sP = sqrt(P);
+        const double X2[3] = {xm, xm + C.phi * sP, xm - C.phi * sP};             // generate_sp :145-169
+        double h[3], Z = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double eta = w[t] / exp(X2[i]);
+            h[i] = (kInvSqrt2Pi * exp(-0.5 * (eta * eta))) * fabs(eta);
+            Z += (i == 0 ? C.wm2_0 : C.wm2_1) * h[i];
+        }
+        if (Z <= 0 || Z < 1e-10) return false;
+        double mean = 0.0;
+        for (int i = 0; i < 3; ++i) mean += ((i == 0 ? C.wm2_0 : C.wm2_1) * X2[i] * h[i]) / Z;
+        double v2 = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double d = X2[i] - mean;
+            v2 += (i == 0 ? C.wm2_0 : C.wm2_1) * ((h[i] / Z) * (d * d));
+        }
+        ll += log(fabs(Z));
+        x = mean;
+        var = v2;
+    }
+    *xmean_last = xm;
+    *LL = ll;
+    return true;
+}
+
+__global__ void k_ukf_forecast(UkfConst C, double a, double l, double q, const double* __restrict__ r, long long n_in,
+                               long long T, double* __restrict__ out, int* err) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    double xm, ll;
+    if (!ukf_pass(C, a, l, q, r + t, n_in, &xm, &ll)) {
+        atomicOr(err, 1);
+        out[t] = __builtin_nan("");
+        return;
+    }
+    out[t] = exp(xm);                                             // forecast.py:12 (Q19)
+}
+
+__global__ void k_ukf_loglik(UkfConst C, const double* __restrict__ prm, long long B, const double* __restrict__ r,
+                             long long N, double* __restrict__ out) {
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xm, ll;
+    const bool ok = ukf_pass(C, prm[3 * b], prm[3 * b + 1], prm[3 * b + 2], r, N, &xm, &ll);
+    out[b] = ok ? ll : -1e10;                                     // estimate.py:270-271
+}
+
+// ------------------------------------------------------------------ KAT
+__global__ void k_special(int fn, TConst tk, const double* __restrict__ x, long long n, double* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = x[i];
+    out[i] = fn == 0 ? stdtrit(tk, v) : (fn == 1 ? ndtri(v) : erf(v));
+}
+
+// ------------------------------------------------------------ host helpers
+struct DevBuf {
+    double* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+int stage_in(const double* src, size_t n, int mem, DevBuf& tmp, const double** dptr) {
+    if (mem == CVQ_MEM_DEVICE) { *dptr = src; return CVQ_OK; }
+    CVQ_HIP_CHECK(hipMalloc((void**)&tmp.p, std::max<size_t>(n, 1) * sizeof(double)));
+    CVQ_HIP_CHECK(hipMemcpy(tmp.p, src, n * sizeof(double), hipMemcpyHostToDevice));
+    *dptr = tmp.p;
+    return CVQ_OK;
+}
+
+int stage_out(double* dst, size_t n, int mem, DevBuf& tmp, double** dptr) {
+    if (mem == CVQ_MEM_DEVICE) { *dptr = dst; return CVQ_OK; }
+    CVQ_HIP_CHECK(hipMalloc((void**)&tmp.p, std::max<size_t>(n, 1) * sizeof(double)));
+    *dptr = tmp.p;
+    return CVQ_OK;
+}
+
+int finish_out(double* dst, size_t n, int mem, const DevBuf& tmp) {
+    CVQ_HIP_CHECK(hipGetLastError());
+    CVQ_HIP_CHECK(hipDeviceSynchronize());
+    if (mem != CVQ_MEM_DEVICE) CVQ_HIP_CHECK(hipMemcpy(dst, tmp.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    return CVQ_OK;
+}
+
+struct DevInt {
+    int* p = nullptr;
+    ~DevInt() { if (p) (void)hipFree(p); }
+};
+
+template <int K>
+void launch_filter(const MsmParams& P, const double* cond, long long n_in, long long T, double* out, int* err) {
+    constexpr int L = Quad<K>::L;
+    const long long threads = T * L;
+    hipLaunchKernelGGL(k_msm_filter<K>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, P, cond, n_in, T,
+                       out, err);
+}
+
+template <int K>
+void launch_msm_ll(const MsmParams* P, long long B, const double* r, long long N, double* out) {
+    constexpr int L = Quad<K>::L;
+    const long long threads = B * L;
+    hipLaunchKernelGGL(k_msm_loglik<K>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, P, B, r, N, out);
+}
+
+int check_device(int device) {
+    int n = 0;
+    CVQ_HIP_CHECK(hipGetDeviceCount(&n));
+    CVQ_REQUIRE(device >= 0 && device < n, CVQ_ERR_INVALID, "device index out of range");
+    CVQ_HIP_CHECK(hipSetDevice(device));
+    return CVQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
+                       const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem) {
+    CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
+    CVQ_REQUIRE(n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "n_in and T must be >= 1");
+    int rc = check_device(device);
+    if (rc) return rc;
+    const MsmParams P = msm_params(k, m0, sigma, b, gamma);
+    const int S = 1 << k;
+    const long long N = n_in + T - 1;
+    DevBuf rin, cond, dout;
+    DevInt err;
+    const double* d_r;
+    double* d_out;
+    if ((rc = stage_in(returns_c, N, mem, rin, &d_r))) return rc;
+    if ((rc = stage_out(out, (size_t)T * S, mem, dout, &d_out))) return rc;
+    CVQ_HIP_CHECK(hipMalloc((void**)&cond.p, (size_t)N * S * sizeof(double)));
+    CVQ_HIP_CHECK(hipMalloc((void**)&err.p, sizeof(int)));
+    CVQ_HIP_CHECK(hipMemset(err.p, 0, sizeof(int)));
+    hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256)), dim3(256), 0, 0, P, S, d_r, N, cond.p);
+    switch (k) {
+        case 1: launch_filter<1>(P, cond.p, n_in, T, d_out, err.p); break;
+        case 2: launch_filter<2>(P, cond.p, n_in, T, d_out, err.p); break;
+        case 3: launch_filter<3>(P, cond.p, n_in, T, d_out, err.p); break;
+        case 4: launch_filter<4>(P, cond.p, n_in, T, d_out, err.p); break;
+        case 5: launch_filter<5>(P, cond.p, n_in, T, d_out, err.p); break;
+        case 6: launch_filter<6>(P, cond.p, n_in, T, d_out, err.p); break;
+        default: launch_filter<7>(P, cond.p, n_in, T, d_out, err.p); break;
+    }
+    if ((rc = finish_out(out, (size_t)T * S, mem, dout))) return rc;
+    int e = 0;
+    CVQ_HIP_CHECK(hipMemcpy(&e, err.p, sizeof(int), hipMemcpyDeviceToHost));
+    CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");
+    return CVQ_OK;
+}
+
+int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double beta, const double* returns_c,
+                           int64_t n_in, int64_t T, double* out, int32_t mem) {
+    CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(omega > 0 && alpha > 0 && beta > 0 && alpha + beta < 1, CVQ_ERR_INVALID,
+                "GARCH parameters must be positive with alpha + beta < 1 (garch/estimation.py:22-38)");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf rin, dout;
+    const double* d_r;
+    double* d_out;
+    if ((rc = stage_in(returns_c, n_in + T - 1, mem, rin, &d_r))) return rc;
+    if ((rc = stage_out(out, T, mem, dout, &d_out))) return rc;
+    hipLaunchKernelGGL(k_garch_forecast, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, omega, alpha, beta, d_r,
+                       n_in, T, d_out);
+    return finish_out(out, T, mem, dout);
+}
+
+int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q, const double* returns_c, int64_t n_in,
+                         int64_t T, double* out, int32_t mem) {
+    CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf rin, dout;
+    DevInt err;
+    const double* d_r;
+    double* d_out;
+    if ((rc = stage_in(returns_c, n_in + T - 1, mem, rin, &d_r))) return rc;
+    if ((rc = stage_out(out, T, mem, dout, &d_out))) return rc;
+    CVQ_HIP_CHECK(hipMalloc((void**)&err.p, sizeof(int)));
+    CVQ_HIP_CHECK(hipMemset(err.p, 0, sizeof(int)));
+    hipLaunchKernelGGL(k_ukf_forecast, dim3((unsigned)((T + 63) / 64)), dim3(64), 0, 0, ukf_const(), a, l, q, d_r, n_in,
+                       T, d_out, err.p);
+    if ((rc = finish_out(out, T, mem, dout))) return rc;
+    int e = 0;
+    CVQ_HIP_CHECK(hipMemcpy(&e, err.p, sizeof(int), hipMemcpyDeviceToHost));
+    CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "UKF normaliser Z < 1e-10 (estimate.py:219-220; reference returns None)");
+    return CVQ_OK;
+}
+
+int32_t cvq_msm_loglik(int32_t device, int32_t k, const double* params, int64_t B, const double* returns, int64_t N,
+                       double* out, int32_t mem) {
+    CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
+    CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
+    int rc = check_device(device);
+    if (rc) return rc;
+    std::vector<double> hp((size_t)B * 4);
+    if (mem == CVQ_MEM_DEVICE) CVQ_HIP_CHECK(hipMemcpy(hp.data(), params, hp.size() * sizeof(double), hipMemcpyDeviceToHost));
+    else std::copy(params, params + hp.size(), hp.begin());
+    std::vector<MsmParams> P((size_t)B);
+    for (long long i = 0; i < B; ++i) P[i] = msm_params(k, hp[4 * i], hp[4 * i + 1], hp[4 * i + 2], hp[4 * i + 3]);
+    MsmParams* dP = nullptr;
+    CVQ_HIP_CHECK(hipMalloc((void**)&dP, P.size() * sizeof(MsmParams)));
+    if (hipMemcpy(dP, P.data(), P.size() * sizeof(MsmParams), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(dP);
+        cvq::set_error("hipMemcpy of MSM parameters failed");
+        return CVQ_ERR_HIP;
+    }
+    DevBuf rin, dout;
+    const double* d_r;
+    double* d_out;
+    if ((rc = stage_in(returns, N, mem, rin, &d_r)) || (rc = stage_out(out, B, mem, dout, &d_out))) {
+        (void)hipFree(dP);
+        return rc;
+    }
+    switch (k) {
+        case 1: launch_msm_ll<1>(dP, B, d_r, N, d_out); break;
+        case 2: launch_msm_ll<2>(dP, B, d_r, N, d_out); break;
+        case 3: launch_msm_ll<3>(dP, B, d_r, N, d_out); break;
+        case 4: launch_msm_ll<4>(dP, B, d_r, N, d_out); break;
+        case 5: launch_msm_ll<5>(dP, B, d_r, N, d_out); break;
+        case 6: launch_msm_ll<6>(dP, B, d_r, N, d_out); break;
+        default: launch_msm_ll<7>(dP, B, d_r, N, d_out); break;
+    }
+    rc = finish_out(out, B, mem, dout);
+    (void)hipFree(dP);
+    return rc;
+}
+
+int32_t cvq_garch_loglik(int32_t device, const double* params, int64_t B, const double* returns, int64_t N,
+                         double* out, int32_t mem) {
+    CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf pin, rin, dout;
+    const double *d_p, *d_r;
+    double* d_out;
+    if ((rc = stage_in(params, (size_t)B * 3, mem, pin, &d_p)) || (rc = stage_in(returns, N, mem, rin, &d_r)) ||
+        (rc = stage_out(out, B, mem, dout, &d_out)))
+        return rc;
+    hipLaunchKernelGGL(k_garch_loglik, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, 0, d_p, B, d_r, N, d_out);
+    return finish_out(out, B, mem, dout);
+}
+
+int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B, const double* returns, int64_t N, double* out,
+                       int32_t mem) {
+    CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf pin, rin, dout;
+    const double *d_p, *d_r;
+    double* d_out;
+    if ((rc = stage_in(params, (size_t)B * 3, mem, pin, &d_p)) || (rc = stage_in(returns, N, mem, rin, &d_r)) ||
+        (rc = stage_out(out, B, mem, dout, &d_out)))
+        return rc;
+    hipLaunchKernelGGL(k_ukf_loglik, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, 0, ukf_const(), d_p, B, d_r, N,
+                       d_out);
+    return finish_out(out, B, mem, dout);
+}
+
+int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int64_t n, double* out, int32_t mem) {
+    CVQ_REQUIRE(x && out && n >= 1, CVQ_ERR_INVALID, "bad argument");
+    CVQ_REQUIRE(fn >= 0 && fn <= 2, CVQ_ERR_INVALID, "fn must be 0 (t.ppf), 1 (norm.ppf) or 2 (erf)");
+    int rc = check_device(device);
+    if (rc) return rc;
+    TConst tk{};
+    if (fn == 0) {
+        CVQ_REQUIRE(nu > 0, CVQ_ERR_INVALID, "nu must be > 0");
+        tk.nu = nu;
+        tk.a = nu / 2;
+        tk.ln_nu = std::log(nu);
+        tk.lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
+        tk.ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
+        tk.ln_tail = tk.ln_k + (nu - 1) / 2 * tk.ln_nu - tk.ln_nu;
+        tk.split = (tk.a + 1.0) / (tk.a + 2.5);
+    }
+    DevBuf xin, dout;
+    const double* d_x;
+    double* d_out;
+    if ((rc = stage_in(x, n, mem, xin, &d_x)) || (rc = stage_out(out, n, mem, dout, &d_out))) return rc;
+    hipLaunchKernelGGL(k_special, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, tk, d_x, n, d_out);
+    return finish_out(out, n, mem, dout);
+}
+
+}  // extern "C"

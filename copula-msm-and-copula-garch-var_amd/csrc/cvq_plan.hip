@@ -1,0 +1,597 @@
+// cvq_plan.hip -- plan lifecycle + C ABI of the quadrature / VaR solve (libcvq.so).
+// See include/cvq.h for the contract and the reference interfaces replaced.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cvq_common.h"
+#include "cvq_quad_kernels.h"
+
+namespace cvq {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+}  // namespace cvq
+
+using namespace cvq;
+
+struct cvq_plan {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    int strategy = CVQ_STRATEGY_PREFIX;
+    double v_cap = 0.0;
+    StaticDev S{};
+    // static device buffers
+    double* d_x = nullptr;
+    double* d_F = nullptr;
+    double* d_phi = nullptr;
+    double* d_uvs = nullptr;
+    int* d_kmax = nullptr;
+    long long* d_off = nullptr;
+    // per-date state
+    long long T = 0, capT = 0;
+    double* d_a = nullptr;       // fbs [T][dim][q] or sigma [T][dim]
+    double* d_pi = nullptr;      // [T][Q]  (GARCH/UKF: ones)
+    double* d_tA = nullptr;      // [T][dim][n]
+    double* d_tB = nullptr;
+    double* d_C = nullptr;       // [T][G]
+    bool tables_valid = false, mass_valid = false;
+    // solve scratch
+    long long capSnap = 0;
+    double* d_snap = nullptr;
+    Header* d_hdr = nullptr;
+    int* d_err = nullptr;
+    long long capIO = 0;
+    double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(T** p, size_t count) {
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (count == 0) count = 1;
+    CVQ_HIP_CHECK(hipMalloc((void**)p, count * sizeof(T)));
+    return CVQ_OK;
+}
+
+int ensure_device(int device) {
+    int n = 0;
+    CVQ_HIP_CHECK(hipGetDeviceCount(&n));
+    CVQ_REQUIRE(device >= 0 && device < n, CVQ_ERR_INVALID, "device index out of range");
+    CVQ_HIP_CHECK(hipSetDevice(device));
+    return CVQ_OK;
+}
+
+// --- bisection budget (calc_var_class.py:278: while any(upper - lower > tol))
+int halvings(double w, double tol) {
+    int k = 0;
+    while (w > tol && k < 1000) { w = w / 2; ++k; }
+    return k;
+}
+
+bool dyadic(double v, int* e) {
+    for (int k = 0; k <= 40; ++k) {
+        const double s = std::ldexp(v, k);
+        if (s == std::floor(s) && std::fabs(s) < 9.0e15) { *e = k; return true; }
+    }
+    return false;
+}
+
+// K = iterations the reference needs for the widest bracket class; exact when
+// every bisection point is exactly representable, else a margin is added and
+// the device verifies convergence (header.error).
+int bisect_budget(const cvq_solve_args& a, bool* exact) {
+    const double br[4][2] = {{a.min_var, a.second_guess_lo}, {a.second_guess_lo, a.first_guess},
+                             {a.second_guess_hi, a.max_var}, {a.first_guess, a.second_guess_hi}};
+    int K = 0;
+    bool ex = true;
+    for (auto& b : br) {
+        const int k = halvings(b[1] - b[0], a.tolerance);
+        K = std::max(K, k);
+        int e0, e1;
+        if (!dyadic(b[0], &e0) || !dyadic(b[1], &e1)) { ex = false; continue; }
+        const double mag = std::max(std::fabs(b[0]), std::fabs(b[1]));
+        const int bits = std::max(e0, e1) + k + (int)std::ceil(std::log2(mag + 1.0)) + 1;
+        if (bits > 52) ex = false;
+    }
+    *exact = ex;
+    return K;
+}
+
+int pick_solve_shape(int nrows, int* tpd, int* rpt) {
+    if (nrows <= 64) { *tpd = 64; *rpt = 1; }
+    else if (nrows <= 128) { *tpd = 64; *rpt = 2; }
+    else if (nrows <= 256) { *tpd = 64; *rpt = 4; }
+    else if (nrows <= 512) { *tpd = 64; *rpt = 8; }
+    else if (nrows <= 1024) { *tpd = 256; *rpt = 4; }
+    else if (nrows <= 4096) { *tpd = 256; *rpt = 16; }
+    else return CVQ_ERR_UNSUPPORTED;
+    return CVQ_OK;
+}
+
+template <int TPD, int RPT>
+void launch_solve_t(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
+    hipLaunchKernelGGL((k_solve_prefix<TPD, RPT>), dim3((unsigned)p->T), dim3(TPD), 0, p->stream, p->S, P, p->d_C,
+                       snaps, hdr);
+}
+template <int TPD, int RPT>
+void launch_slab_t(cvq_plan* p, const double* bounds, double* out) {
+    hipLaunchKernelGGL((k_slab_prefix<TPD, RPT>), dim3((unsigned)p->T), dim3(TPD), 0, p->stream, p->S, p->d_C,
+                       bounds, out);
+}
+
+int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
+    int tpd, rpt;
+    CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
+                "prefix solve supports at most 4096 rows (3-D n <= 64)");
+    if (tpd == 64 && rpt == 1) launch_solve_t<64, 1>(p, P, snaps, hdr);
+    else if (tpd == 64 && rpt == 2) launch_solve_t<64, 2>(p, P, snaps, hdr);
+    else if (tpd == 64 && rpt == 4) launch_solve_t<64, 4>(p, P, snaps, hdr);
+    else if (tpd == 64 && rpt == 8) launch_solve_t<64, 8>(p, P, snaps, hdr);
+    else if (tpd == 256 && rpt == 4) launch_solve_t<256, 4>(p, P, snaps, hdr);
+    else launch_solve_t<256, 16>(p, P, snaps, hdr);
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+int launch_slab(cvq_plan* p, const double* bounds, double* out) {
+    int tpd, rpt;
+    CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
+                "prefix slab supports at most 4096 rows (3-D n <= 64)");
+    if (tpd == 64 && rpt == 1) launch_slab_t<64, 1>(p, bounds, out);
+    else if (tpd == 64 && rpt == 2) launch_slab_t<64, 2>(p, bounds, out);
+    else if (tpd == 64 && rpt == 4) launch_slab_t<64, 4>(p, bounds, out);
+    else if (tpd == 64 && rpt == 8) launch_slab_t<64, 8>(p, bounds, out);
+    else if (tpd == 256 && rpt == 4) launch_slab_t<256, 4>(p, bounds, out);
+    else launch_slab_t<256, 16>(p, bounds, out);
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+template <int COP, bool MSM>
+void launch_tables_t(cvq_plan* p) {
+    const long long total = p->T * p->S.dim * p->S.n;
+    const unsigned blocks = (unsigned)((total + 255) / 256);
+    hipLaunchKernelGGL((k_tables<COP, MSM>), dim3(blocks), dim3(256), 0, p->stream, p->S, p->T, p->d_a, p->d_tA,
+                       p->d_tB);
+}
+
+size_t mass_lds_bytes(const StaticDev& S) {
+    return sizeof(double) * (4 * (size_t)S.n + 2 * (size_t)S.q * S.n + 2 * (size_t)S.q * S.q + S.Q);
+}
+
+template <int COP, bool MSM, int DIM>
+void launch_mass_t(cvq_plan* p) {
+    const dim3 grid((unsigned)p->T, DIM == 3 ? (unsigned)p->S.n : 1u);
+    hipLaunchKernelGGL((k_mass<COP, MSM, DIM>), grid, dim3(256), mass_lds_bytes(p->S), p->stream, p->S, p->d_tA,
+                       p->d_tB, p->d_pi, p->d_C);
+}
+
+template <int COP>
+void launch_cop(cvq_plan* p, bool tables) {
+    const bool msm = p->S.model == CVQ_MSM;
+    if (tables) {
+        if (msm) launch_tables_t<COP, true>(p); else launch_tables_t<COP, false>(p);
+        return;
+    }
+    if (p->S.dim == 2) {
+        if (msm) launch_mass_t<COP, true, 2>(p); else launch_mass_t<COP, false, 2>(p);
+    } else if constexpr (COP != CVQ_PLACKETT) {
+        if (msm) launch_mass_t<COP, true, 3>(p); else launch_mass_t<COP, false, 3>(p);
+    }
+}
+
+int dispatch_cop(cvq_plan* p, bool tables) {
+    switch (p->S.copula) {
+        case CVQ_GAUSSIAN: launch_cop<CVQ_GAUSSIAN>(p, tables); break;
+        case CVQ_STUDENT: launch_cop<CVQ_STUDENT>(p, tables); break;
+        default: launch_cop<CVQ_PLACKETT>(p, tables); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+int ensure_mass(cvq_plan* p) {
+    CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));
+    if (!p->tables_valid) {
+        int rc = dispatch_cop(p, true);
+        if (rc) return rc;
+        p->tables_valid = true;
+        p->mass_valid = false;
+    }
+    if (!p->mass_valid) {
+        int rc = dispatch_cop(p, false);
+        if (rc) return rc;
+        p->mass_valid = true;
+    }
+    return CVQ_OK;
+}
+
+SolveConst solve_const(const cvq_solve_args& a, int K) {
+    SolveConst P;
+    P.obj = a.obj_var;
+    P.fg = a.first_guess;
+    P.sg0 = a.second_guess_lo;
+    P.sg1 = a.second_guess_hi;
+    P.vmin = a.min_var;
+    P.vmax = a.max_var;
+    P.lower = a.lower;
+    P.tol = a.tolerance;
+    P.K = K;
+    P.stride = K + 1;
+    return P;
+}
+
+int check_args(const cvq_plan* p, const cvq_solve_args* a) {
+    CVQ_REQUIRE(a != nullptr, CVQ_ERR_INVALID, "solve args is NULL");
+    const double top = std::max({a->first_guess, a->second_guess_lo, a->second_guess_hi, a->max_var, a->min_var,
+                                 a->lower});
+    CVQ_REQUIRE(!(top > p->v_cap), CVQ_ERR_RANGE,
+                "a VaR level in the solve arguments exceeds the plan's v_cap");
+    CVQ_REQUIRE(a->tolerance > 0.0, CVQ_ERR_INVALID, "tolerance must be > 0");
+    return CVQ_OK;
+}
+
+int ensure_snap(cvq_plan* p, long long need) {
+    if (need > p->capSnap) {
+        int rc = dev_alloc(&p->d_snap, (size_t)need);
+        if (rc) return rc;
+        p->capSnap = need;
+    }
+    return CVQ_OK;
+}
+
+int ensure_io(cvq_plan* p, long long need) {
+    if (need > p->capIO) {
+        int rc = dev_alloc(&p->d_io, (size_t)need);
+        if (rc) return rc;
+        p->capIO = need;
+    }
+    return CVQ_OK;
+}
+
+// Invert a symmetric dim x dim matrix (2 or 3) by cofactors; returns det.
+double invert(const double* R, int d, double* Ri) {
+    if (d == 2) {
+        const double det = R[0] * R[3] - R[1] * R[2];
+        Ri[0] = R[3] / det; Ri[1] = -R[1] / det; Ri[2] = -R[2] / det; Ri[3] = R[0] / det;
+        return det;
+    }
+    const double a = R[0], b = R[1], c = R[2], d_ = R[3], e = R[4], f = R[5], g = R[6], h = R[7], i = R[8];
+    const double A = e * i - f * h, B = -(d_ * i - f * g), C = d_ * h - e * g;
+    const double det = a * A + b * B + c * C;
+    Ri[0] = A / det; Ri[1] = -(b * i - c * h) / det; Ri[2] = (b * f - c * e) / det;
+    Ri[3] = B / det; Ri[4] = (a * i - c * g) / det;  Ri[5] = -(a * f - c * d_) / det;
+    Ri[6] = C / det; Ri[7] = -(a * h - b * g) / det; Ri[8] = (a * e - b * d_) / det;
+    return det;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* cvq_last_error(void) { return g_err.c_str(); }
+int32_t cvq_version(void) { return 10000; }
+
+int32_t cvq_device_count(int32_t* count) {
+    CVQ_REQUIRE(count != nullptr, CVQ_ERR_INVALID, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
+    CVQ_REQUIRE(s != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    CVQ_REQUIRE(s->model >= CVQ_MSM && s->model <= CVQ_UKF, CVQ_ERR_INVALID, "unknown model kind");
+    CVQ_REQUIRE(s->copula >= CVQ_GAUSSIAN && s->copula <= CVQ_PLACKETT, CVQ_ERR_INVALID, "unknown copula kind");
+    CVQ_REQUIRE(s->dim == 2 || s->dim == 3, CVQ_ERR_UNSUPPORTED, "dim must be 2 or 3");
+    CVQ_REQUIRE(!(s->copula == CVQ_PLACKETT && s->dim != 2), CVQ_ERR_UNSUPPORTED,
+                "Plackett copula is only defined for 2-dimensional marginals (plackett.py:20-21)");
+    CVQ_REQUIRE(s->n >= 2 && s->n <= 512, CVQ_ERR_UNSUPPORTED, "num_points must be in [2, 512]");
+    CVQ_REQUIRE(s->q >= 1 && s->q <= kMaxQ, CVQ_ERR_UNSUPPORTED, "q (unique vol states) must be in [1, 8]");
+    int Q = 1;
+    for (int d = 0; d < s->dim; ++d) Q *= s->q;
+    CVQ_REQUIRE(s->n_combos == Q, CVQ_ERR_INVALID, "n_combos must equal q**dim");
+    CVQ_REQUIRE(s->model == CVQ_MSM || s->q == 1, CVQ_ERR_INVALID, "GARCH/UKF plans have q == 1");
+    CVQ_REQUIRE(s->x_values && s->step && s->densities && s->combos && s->weights && s->copula_params,
+                CVQ_ERR_INVALID, "NULL static table");
+    CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
+    CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
+    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX, CVQ_ERR_UNSUPPORTED, "only the PREFIX strategy is built");
+    for (int l = 0; l < Q; ++l) {             // create_vol_combinations ij order (msm_estimation.py:384)
+        int rem = l;
+        for (int d = s->dim - 1; d >= 0; --d) {
+            CVQ_REQUIRE(s->combos[l * s->dim + d] == rem % s->q, CVQ_ERR_INVALID,
+                        "combos must be the ij-meshgrid index combinations");
+            rem /= s->q;
+        }
+    }
+    for (int i = 1; i < s->n; ++i)
+        CVQ_REQUIRE(s->x_values[i] > s->x_values[i - 1], CVQ_ERR_INVALID, "x_values must be increasing");
+    int rc = ensure_device(device);
+    if (rc) return rc;
+
+    cvq_plan* p = new cvq_plan();
+    p->device = device;
+    p->strategy = s->strategy;
+    p->v_cap = s->v_cap;
+    StaticDev& S = p->S;
+    S.model = s->model;
+    S.copula = s->copula;
+    S.dim = s->dim;
+    S.n = s->n;
+    S.q = s->q;
+    S.Q = Q;
+    S.nrows = s->dim == 2 ? s->n : s->n * s->n;
+    S.w0 = s->weights[0];
+    S.w1 = s->weights[1];
+    S.w2 = s->dim == 3 ? s->weights[2] : 0.0;
+
+    // copula constants, computed as the reference does on the host
+    const int d = s->dim;
+    const double* cp = s->copula_params;
+    if (s->copula == CVQ_PLACKETT) {
+        CVQ_REQUIRE(s->n_copula_params >= 1, CVQ_ERR_INVALID, "Plackett needs theta");
+        S.theta = cp[0];
+    } else {
+        const int nrho = d * (d - 1) / 2;
+        const int base = s->copula == CVQ_STUDENT ? 1 : 0;
+        CVQ_REQUIRE(s->n_copula_params == base + nrho, CVQ_ERR_INVALID, "wrong copula parameter count");
+        double R[9];
+        int k = 0;
+        for (int i = 0; i < d; ++i) R[i * d + i] = 1.0;
+        for (int i = 0; i < d; ++i)                 // triu / tril fill (student_estimation.py:50-54)
+            for (int j = i + 1; j < d; ++j) { R[i * d + j] = R[j * d + i] = cp[base + k]; ++k; }
+        const double det = invert(R, d, S.Ri);
+        if (s->copula == CVQ_STUDENT) {
+            const double nu = cp[0];
+            CVQ_REQUIRE(nu > 0.0, CVQ_ERR_INVALID, "nu must be > 0");
+            S.nu = nu;
+            S.inv_nu = 1.0 / nu;
+            S.term1 = std::tgamma((nu + d) / 2) /
+                      (std::tgamma(nu / 2) * std::pow(nu * M_PI, d / 2.0) * std::sqrt(det));   // student.py:138
+            S.g_uni = std::tgamma((nu + 1) / 2) / (std::sqrt(nu * M_PI) * std::tgamma(nu / 2)); // :164
+            S.node_ex = -(nu + d) / 2;
+            S.uni_ex = -(nu + 1) / 2;
+            const double m2 = -2.0 * S.node_ex;
+            S.node_m = (m2 == std::floor(m2) && m2 <= 128.0) ? (int)m2 : -1;
+            TConst& tk = S.tk;
+            tk.nu = nu;
+            tk.a = nu / 2;
+            tk.ln_nu = std::log(nu);
+            tk.lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
+            tk.ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
+            tk.ln_tail = tk.ln_k + (nu - 1) / 2 * tk.ln_nu - tk.ln_nu;
+            tk.split = (tk.a + 1.0) / (tk.a + 2.5);
+        } else {
+            S.term1 = 1 / (std::sqrt(std::pow(2 * M_PI, d) * det));                              // gaussian.py:107
+        }
+    }
+
+    // static tables
+    const int n = s->n, q = s->q;
+    std::vector<double> F((size_t)d * q * n);
+    for (int c = 0; c < d; ++c)                     // axis c uses densities[(c-1) mod dim] (Q5)
+        for (int sidx = 0; sidx < q; ++sidx)
+            for (int i = 0; i < n; ++i)
+                F[((size_t)c * q + sidx) * n + i] =
+                    s->densities[((size_t)((c - 1 + d) % d) * q + sidx) * n + i] * s->step[i];
+    // geometry: reachable inner nodes per row at v_cap (create_grids.py:104-108)
+    std::vector<int> kmax(S.nrows);
+    std::vector<long long> off(S.nrows);
+    long long G = 0;
+    const double* x = s->x_values;
+    for (int r = 0; r < S.nrows; ++r) {
+        double lev;
+        if (d == 2) lev = x[r] * S.w1;
+        else lev = x[r / n] * S.w1 + x[r % n] * S.w2;
+        const double g = (s->v_cap - lev) / S.w0;
+        int k = 0;
+        for (int j = 1; j < n; ++j) if (x[j] <= g) k = j;
+        kmax[r] = k;
+        off[r] = G;
+        G += k;
+    }
+    S.G = G;
+    rc = 0;
+    do {
+        if ((rc = dev_alloc(&p->d_x, n))) break;
+        if ((rc = dev_alloc(&p->d_F, F.size()))) break;
+        if ((rc = dev_alloc(&p->d_kmax, kmax.size()))) break;
+        if ((rc = dev_alloc(&p->d_off, off.size()))) break;
+        if ((rc = dev_alloc(&p->d_hdr, 1))) break;
+        if ((rc = dev_alloc(&p->d_err, 4))) break;
+    } while (0);
+    if (rc) { cvq_plan_destroy(p); return rc; }
+    hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+    p->stream = p->own_stream;
+    e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_kmax, kmax.data(), kmax.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_off, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+    S.x = p->d_x;
+    S.F = p->d_F;
+    S.kmax = p->d_kmax;
+    S.off = p->d_off;
+    if (s->model == CVQ_MSM) {
+        if ((rc = dev_alloc(&p->d_uvs, (size_t)d * q)) || (rc = dev_alloc(&p->d_phi, (size_t)d * q * n))) {
+            cvq_plan_destroy(p);
+            return rc;
+        }
+        e = hipMemcpy(p->d_uvs, s->vol_states, (size_t)d * q * sizeof(double), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+        const int total = d * q * n;
+        hipLaunchKernelGGL(k_phi, dim3((total + 255) / 256), dim3(256), 0, p->stream, S, p->d_uvs, p->d_phi);
+        e = hipStreamSynchronize(p->stream);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+        S.phi = p->d_phi;
+    }
+    CVQ_REQUIRE(mass_lds_bytes(S) <= 64 * 1024, CVQ_ERR_UNSUPPORTED, "quadrature tables exceed 64 KiB of LDS");
+    *out = p;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_destroy(cvq_plan* p) {
+    if (!p) return CVQ_OK;
+    (void)hipSetDevice(p->device);
+    if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
+    for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_kmax,
+                    (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
+                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io})
+        if (b) (void)hipFree(b);
+    if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    delete p;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_set_stream(cvq_plan* p, void* s) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    p->stream = s ? (hipStream_t)s : p->own_stream;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_info(const cvq_plan* p, int64_t* reach, int32_t* rows) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    if (reach) *reach = p->S.G;
+    if (rows) *rows = p->S.nrows;
+    return CVQ_OK;
+}
+
+int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, int32_t mem) {
+    CVQ_REQUIRE(p != nullptr && a != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(T > 0, CVQ_ERR_INVALID, "T must be > 0");
+    CVQ_REQUIRE(p->S.model != CVQ_MSM || b != nullptr, CVQ_ERR_INVALID, "MSM needs the forecast combinations");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));
+    const StaticDev& S = p->S;
+    const size_t na = (size_t)T * S.dim * (S.model == CVQ_MSM ? S.q : 1);
+    const size_t npi = (size_t)T * S.Q;
+    if (T > p->capT) {
+        int rc;
+        if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi)) ||
+            (rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)) ||
+            (rc = dev_alloc(&p->d_C, (size_t)T * S.G)))
+            return rc;
+        p->capT = T;
+    }
+    p->T = T;
+    const hipMemcpyKind kind = mem == CVQ_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_a, a, na * sizeof(double), kind, p->stream));
+    if (S.model == CVQ_MSM) {
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, b, npi * sizeof(double), kind, p->stream));
+    } else {
+        std::vector<double> ones(npi, 1.0);
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), npi * sizeof(double), hipMemcpyHostToDevice, p->stream));
+        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    }
+    if (mem != CVQ_MEM_DEVICE) CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    p->tables_valid = false;
+    p->mass_valid = false;
+    return CVQ_OK;
+}
+
+int32_t cvq_slab(cvq_plan* p, const double* bounds, double* out, int32_t mem) {
+    CVQ_REQUIRE(p != nullptr && bounds != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
+    if (mem != CVQ_MEM_DEVICE) {
+        for (long long t = 0; t < 2 * p->T; ++t)
+            CVQ_REQUIRE(!(bounds[t] > p->v_cap), CVQ_ERR_RANGE, "a bound exceeds the plan's v_cap");
+    }
+    int rc = ensure_mass(p);
+    if (rc) return rc;
+    if (mem == CVQ_MEM_DEVICE) return launch_slab(p, bounds, out);
+    if ((rc = ensure_io(p, 3 * p->T))) return rc;
+    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_io, bounds, 2 * p->T * sizeof(double), hipMemcpyHostToDevice, p->stream));
+    if ((rc = launch_slab(p, p->d_io, p->d_io + 2 * p->T))) return rc;
+    CVQ_HIP_CHECK(hipMemcpyAsync(out, p->d_io + 2 * p->T, p->T * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    return CVQ_OK;
+}
+
+int32_t cvq_snap_stride(const cvq_solve_args* a, int32_t* stride) {
+    CVQ_REQUIRE(a != nullptr && stride != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    bool exact;
+    int K = bisect_budget(*a, &exact);
+    if (!exact) K += 2;
+    CVQ_REQUIRE(K <= kMaxIters, CVQ_ERR_UNSUPPORTED, "bisection needs more than 62 iterations");
+    *stride = K + 1;
+    return CVQ_OK;
+}
+
+int32_t cvq_solve_local(cvq_plan* p, const cvq_solve_args* a, void* d_header, double* d_snaps) {
+    CVQ_REQUIRE(p != nullptr && d_header != nullptr && d_snaps != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    int rc = check_args(p, a);
+    if (rc) return rc;
+    int32_t stride;
+    if ((rc = cvq_snap_stride(a, &stride))) return rc;
+    if ((rc = ensure_mass(p))) return rc;
+    CVQ_HIP_CHECK(hipMemsetAsync(d_header, 0, sizeof(Header), p->stream));
+    return launch_solve(p, solve_const(*a, stride - 1), d_snaps, (Header*)d_header);
+}
+
+int32_t cvq_solve_finalize(cvq_plan* p, const cvq_solve_args* a, const void* d_headers, int32_t n_ranks,
+                           const double* d_snaps, int64_t dates_per_rank, int64_t T_total, double* d_var) {
+    CVQ_REQUIRE(p != nullptr && a != nullptr && d_headers && d_snaps && d_var, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(n_ranks >= 1 && T_total <= (int64_t)n_ranks * dates_per_rank, CVQ_ERR_INVALID,
+                "T_total exceeds n_ranks * dates_per_rank");
+    int32_t stride;
+    int rc = cvq_snap_stride(a, &stride);
+    if (rc) return rc;
+    CVQ_HIP_CHECK(hipSetDevice(p->device));
+    const unsigned blocks = (unsigned)std::max<long long>(1, (T_total + 255) / 256);
+    hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)d_headers, n_ranks,
+                       d_snaps, (long long)T_total, stride, stride - 1, a->ptf_mean, d_var, p->d_err);
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t* iters_out, int32_t mem) {
+    CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    int rc = check_args(p, a);
+    if (rc) return rc;
+    if ((rc = ensure_mass(p))) return rc;
+    bool exact;
+    int K = bisect_budget(*a, &exact);
+    if (!exact) K += 2;
+    for (;;) {
+        CVQ_REQUIRE(K <= kMaxIters, CVQ_ERR_NUMERIC, "bisection did not converge within 62 iterations");
+        const int stride = K + 1;
+        if ((rc = ensure_snap(p, p->T * stride))) return rc;
+        double* d_var = var_out;
+        if (mem != CVQ_MEM_DEVICE) {
+            if ((rc = ensure_io(p, p->T))) return rc;
+            d_var = p->d_io;
+        }
+        CVQ_HIP_CHECK(hipMemsetAsync(p->d_hdr, 0, sizeof(Header), p->stream));
+        if ((rc = launch_solve(p, solve_const(*a, K), p->d_snap, p->d_hdr))) return rc;
+        const unsigned blocks = (unsigned)((p->T + 255) / 256);
+        hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)p->d_hdr, 1,
+                           (const double*)p->d_snap, p->T, stride, K, a->ptf_mean, d_var, p->d_err);
+        CVQ_HIP_CHECK(hipGetLastError());
+        if (mem == CVQ_MEM_DEVICE && iters_out == nullptr) return CVQ_OK;
+        int err[4] = {0, 0, 0, 0};
+        CVQ_HIP_CHECK(hipMemcpyAsync(err, p->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+        if (err[0]) { K += 4; continue; }          // a date needed more than K iterations: widen
+        if (iters_out) *iters_out = err[1];
+        if (mem != CVQ_MEM_DEVICE) {
+            CVQ_HIP_CHECK(hipMemcpy(var_out, d_var, p->T * sizeof(double), hipMemcpyDeviceToHost));
+        }
+        return CVQ_OK;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,471 @@
+// cvq_quad_kernels.h -- gfx950 kernels of the copula quadrature + VaR solve.
+//
+// Reference path (Nassim-cha/copula-MSM-and-copula-Garch-VaR @ 2024-11-25):
+//   calc_var            utils/calc_var_class.py:95-177, bisection :250-309, adjust :214-248
+//   compute_integral    utils/calc_var_class.py:179-212 -> utils/calc_integral/calc_integral.py:8-225
+//   nested grid         utils/calc_integral/create_grids.py:6-240 (membership :102-108, :127; Q5/Q6)
+//   integrands          utils/calc_integral/integration_functions/{msm,garch}_integration_function.py
+//   copula densities    copulas/{student,gaussian,plackett}/*.py
+//
+// MI355X design: the special functions depend only on (date, axis,
+// 1-D grid index), so k_tables evaluates them once per table entry; a node of
+// the nested grid then costs a quadratic form, one power and a short W
+// contraction.  Rows of the innermost axis are processed one wavefront per
+// row with an in-register inclusive scan; the solve walks the bisection with
+// per-row binary searches on an LDS copy of the grid.
+#pragma once
+#include "cvq_common.h"
+
+namespace cvq {
+
+constexpr double kInvSqrt2 = 1.4142135623730951;      // np.sqrt(2): divided by, as utils.py:20
+constexpr double kInvSqrt2Pi = 0.3989422804014327;    // 1 / np.sqrt(2 * np.pi)
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// -------------------------------------------------------- static Phi (MSM only)
+// phi[d][s][i] = 0.5 * (1 + erf((x_i / sigma_{d,s}) / sqrt 2))  (msm_integration_function.py:32-36)
+__global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __restrict__ phi) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = S.dim * S.q * S.n;
+    if (idx >= total) return;
+    const int i = idx % S.n;
+    const int ds = idx / S.n;
+    const double xs = S.x[i] / uvs[ds];
+    phi[idx] = 0.5 * (1.0 + erf(xs / kInvSqrt2));
+}
+
+// ---------------------------------------------------------------- k_tables
+// One thread per (date t, axis d, grid index i):
+//   u   = marginal CDF  (MSM: sum_s f_t[d,s] Phi(x/sigma_{d,s}); GARCH/UKF: Phi(x/sigma_t,d))
+//   A   = z = t.ppf(u, nu) | norm.ppf(u)        (Plackett: A = u)
+//   B   = pdf / univariate-copula-margin-pdf      (MSM: pdf = 1; Plackett: B = pdf)
+// Layout [T][dim][n], coalesced along i.
+template <int COP, bool MSM>
+__global__ __launch_bounds__(256) void k_tables(StaticDev S, long long T, const double* __restrict__ a,
+                                                double* __restrict__ tA, double* __restrict__ tB) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = T * S.dim * S.n;
+    if (idx >= total) return;
+    const int i = (int)(idx % S.n);
+    const long long td = idx / S.n;
+    const int d = (int)(td % S.dim);
+    double u, pdf = 1.0;
+    if (MSM) {
+        const double* f = a + td * S.q;
+        const double* ph = S.phi + (size_t)d * S.q * S.n + i;
+        double acc = f[0] * ph[0];
+        for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
+        u = acc;
+    } else {
+        const double sig = a[td];
+        const double xs = S.x[i] / sig;                         // garch_integration_function.py:31
+        u = 0.5 * (1.0 + erf(xs / kInvSqrt2));                   // :33
+        pdf = (kInvSqrt2Pi * exp(-0.5 * (xs * xs))) / sig;       // :38
+    }
+    double A, B;
+    if (COP == CVQ_PLACKETT) {
+        A = u;
+        B = pdf;
+    } else {
+        double z, uni;
+        if (COP == CVQ_STUDENT) {
+            z = stdtrit(S.tk, u);                                // student.py:102
+            uni = isfinite(z) ? S.g_uni * pow(1.0 + (z * z) / S.nu, S.uni_ex) : 0.0;   // :164-172
+        } else {
+            z = ndtri(u);                                        // gaussian.py:44
+            uni = kInvSqrt2Pi * exp(-0.5 * (z * z));             // gaussian.py:82
+        }
+        A = z;
+        B = (1.0 / uni) * pdf;
+    }
+    tA[idx] = A;
+    tB[idx] = B;
+}
+
+// ---------------------------------------------------------------- node value
+// Row context: everything about a node that depends only on its outer indices.
+struct RowCtx {
+    double z0, z1;      // outer-axis table values (z, or u for Plackett)
+    double p0, p1, p2;  // outer part of y = z^T R^-1 (student.py:136 order)
+    double B;           // product of outer B factors
+    bool fin;           // all outer z finite (student.py:133)
+};
+
+template <int COP, bool MSM, int DIM>
+__device__ __forceinline__ double node_value(const StaticDev& S, const RowCtx& r, double zc, double Bc,
+                                             double W) {
+    double c;
+    if (COP == CVQ_PLACKETT) {
+        const double u = r.z0, v = zc, th = S.theta;               // plackett.py:66-69 (Q11)
+        const double num = th * (1.0 + (th - 1.0) * (u + v - 2.0 * u * v));
+        double den = (1.0 + (th - 1.0) * (u + v)) * (1.0 + (th - 1.0) * (1.0 - u - v));
+        den = den * den;
+        c = (num / den) * (r.B * Bc);
+    } else {
+        double qf;
+        if (DIM == 2) {
+            const double y0 = r.p0 + zc * S.Ri[2];
+            const double y1 = r.p1 + zc * S.Ri[3];
+            qf = y0 * r.z0 + y1 * zc;
+        } else {
+            const double y0 = r.p0 + zc * S.Ri[6];
+            const double y1 = r.p1 + zc * S.Ri[7];
+            const double y2 = r.p2 + zc * S.Ri[8];
+            qf = (y0 * r.z0 + y1 * r.z1) + y2 * zc;
+        }
+        double mv;
+        if (COP == CVQ_STUDENT) {
+            const bool fin = r.fin && isfinite(zc);
+            mv = fin ? S.term1 * pow_node(1.0 + qf * S.inv_nu, S.node_m, S.node_ex) : 0.0;   // :133-141
+        } else {
+            mv = S.term1 * exp(-0.5 * qf);                         // gaussian.py:105-113
+        }
+        c = mv * (r.B * Bc);                                       // c / prod(uni) [* prod(pdf)]
+    }
+    if (MSM) return c * W;                                          // no NaN guard (Q15)
+    return nan_to_num(c) * W;                                       // garch_integration_function.py:45-50
+}
+
+template <int COP, int DIM>
+__device__ __forceinline__ RowCtx make_row(const StaticDev& S, double z0, double z1, double B) {
+    RowCtx r;
+    r.z0 = z0;
+    r.z1 = z1;
+    r.B = B;
+    if (COP == CVQ_PLACKETT) {
+        r.p0 = r.p1 = r.p2 = 0.0;
+        r.fin = true;
+    } else if (DIM == 2) {
+        r.p0 = z0 * S.Ri[0];
+        r.p1 = z0 * S.Ri[1];
+        r.p2 = 0.0;
+        r.fin = isfinite(z0);
+    } else {
+        r.p0 = z0 * S.Ri[0] + z1 * S.Ri[3];
+        r.p1 = z0 * S.Ri[1] + z1 * S.Ri[4];
+        r.p2 = z0 * S.Ri[2] + z1 * S.Ri[5];
+        r.fin = isfinite(z0) && isfinite(z1);
+    }
+    return r;
+}
+
+// ------------------------------------------------- MSM / Delta-product weights
+// W(node) = sum_l pi_t[l] Delta[node, l]  with  Delta = prod_c F_c(combo_c, i_c)
+// (create_grids.py:121,143; Q5 rotation baked into F; Q6: in 3-D the axis-0
+// factor only where i1 == 0).  Contracted as G_row[b] (outer axes) . F_inner(b, col).
+// LDS block used by k_mass / k_solve_direct:
+struct WeightsLds {
+    double* cF;   // [q][n]  inner-axis F
+    double* rG;   // [n][q]  per outer row (2-D: i0; 3-D: i1 with fixed i0)
+    double* H;    // 3-D: [2][q][q]
+    double* pi;   // [Q]
+};
+
+// Fill rG for the n outer rows of this block.  2-D: rows are i0.  3-D: block i0, rows i1.
+__device__ inline void build_row_weights(const StaticDev& S, const WeightsLds& L, int i0_block, int dim) {
+    const int n = S.n, q = S.q;
+    if (dim == 3) {
+        for (int bc = threadIdx.x; bc < q * q; bc += blockDim.x) {
+            double hw = 0.0, ho = 0.0;
+            for (int a = 0; a < q; ++a) {
+                const double p = L.pi[a * q * q + bc];
+                hw += p * S.F[(size_t)a * n + i0_block];         // axis-0 factor F_0(a, i0)
+                ho += p;                                         // axis-0 factor reset to 1 (Q6)
+            }
+            L.H[bc] = hw;
+            L.H[q * q + bc] = ho;
+        }
+        __syncthreads();
+    }
+    for (int rb = threadIdx.x; rb < n * q; rb += blockDim.x) {
+        const int r = rb / q, b = rb % q;
+        double g = 0.0;
+        if (dim == 2) {
+            for (int a = 0; a < q; ++a) g += L.pi[a * q + b] * S.F[(size_t)a * n + r];
+        } else {
+            const double* H = L.H + (r == 0 ? 0 : q * q);
+            for (int bb = 0; bb < q; ++bb) g += H[bb * q + b] * S.F[((size_t)q + bb) * n + r];
+        }
+        L.rG[rb] = g;
+    }
+}
+
+// ------------------------------------------------------------------ k_mass
+// PREFIX strategy: C[t][off[r] + j - 1] = sum_{j' <= j} node(t, r, j') for every
+// reachable node (level <= v_cap).  grid = (T, dim == 3 ? n : 1), 256 threads,
+// one wavefront per row, 64 columns per step, inclusive scan in registers.
+template <int COP, bool MSM, int DIM>
+__global__ __launch_bounds__(256) void k_mass(StaticDev S, const double* __restrict__ tA,
+                                              const double* __restrict__ tB, const double* __restrict__ pi,
+                                              double* __restrict__ C) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int QM = MSM ? kMaxQ : 1;
+    const int n = S.n, q = S.q;
+    const long long t = blockIdx.x;
+    const int blk = blockIdx.y;
+    double* cA = lds;
+    double* cB = cA + n;
+    double* rA = cB + n;
+    double* rB = rA + n;
+    WeightsLds L;
+    L.cF = rB + n;
+    L.rG = L.cF + (size_t)q * n;
+    L.H = L.rG + (size_t)q * n;
+    L.pi = L.H + 2 * q * q;
+    const int inner = DIM - 1, rowaxis = DIM - 2;
+    const double* At = tA + t * S.dim * n;
+    const double* Bt = tB + t * S.dim * n;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        cA[j] = At[inner * n + j];
+        cB[j] = Bt[inner * n + j];
+        rA[j] = At[rowaxis * n + j];
+        rB[j] = Bt[rowaxis * n + j];
+        for (int b = 0; b < q; ++b) L.cF[b * n + j] = S.F[((size_t)inner * q + b) * n + j];
+    }
+    for (int l = threadIdx.x; l < S.Q; l += blockDim.x) L.pi[l] = pi[t * S.Q + l];
+    __syncthreads();
+    build_row_weights(S, L, blk, DIM);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const double z0fix = (DIM == 3) ? At[blk] : 0.0;
+    const double B0fix = (DIM == 3) ? Bt[blk] : 1.0;
+    double* Cd = C + t * S.G;
+    for (int rl = wave; rl < n; rl += nw) {
+        const int r = (DIM == 2) ? rl : blk * n + rl;
+        const int km = S.kmax[r];
+        if (km == 0) continue;
+        double* Cr = Cd + S.off[r];
+        const RowCtx ctx = (DIM == 2) ? make_row<COP, DIM>(S, rA[rl], 0.0, rB[rl])
+                                      : make_row<COP, DIM>(S, z0fix, rA[rl], B0fix * rB[rl]);
+        double G[QM];
+#pragma unroll
+        for (int b = 0; b < QM; ++b) G[b] = (b < q) ? L.rG[rl * q + b] : 0.0;
+        double carry = 0.0;
+        for (int j0 = 1; j0 <= km; j0 += 64) {
+            const int j = j0 + lane;
+            double v = 0.0;
+            if (j <= km) {
+                double W = 0.0;
+#pragma unroll
+                for (int b = 0; b < QM; ++b)
+                    if (b < q) W += G[b] * L.cF[b * n + j];
+                v = node_value<COP, MSM, DIM>(S, ctx, cA[j], cB[j], W);
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const double y = __shfl_up(v, o, 64);
+                if (lane >= o) v += y;
+            }
+            v += carry;
+            if (j <= km) Cr[j - 1] = v;
+            carry = __shfl(v, 63, 64);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ solve
+// Team of TPD threads per date; thread owns rows r = tid + i*TPD (i < RPT).
+template <int TPD>
+struct TeamReduce {
+    __device__ static double sum(double v, double* red) {
+        v = wave_sum(v);
+        if (TPD == 64) return v;
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        __syncthreads();
+        if (lane == 0) red[wave] = v;
+        __syncthreads();
+        double s = red[0];
+#pragma unroll
+        for (int w = 1; w < TPD / 64; ++w) s += red[w];
+        return s;
+    }
+};
+
+// count of inner nodes j in [1, kmax] with x_j <= g, searched in [klo, khi]
+// (x_{klo} <= g is known true, or klo == 0).  create_grids.py:104-108.
+__device__ __forceinline__ int count_le(const double* sx, double g, int klo, int khi) {
+    int lo = klo, hi = khi;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sx[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ double row_level(const StaticDev& S, const double* sx, int r) {
+    // np.sum(previous_points * weights[1:]) (integration_algo.py:20)
+    if (S.dim == 2) return sx[r] * S.w1;
+    const int i0 = r / S.n, i1 = r % S.n;
+    return sx[i0] * S.w1 + sx[i1] * S.w2;
+}
+
+template <int TPD, int RPT>
+struct SolveTeam {
+    const StaticDev& S;
+    const double* sx;
+    const double* Cd;      // this date's prefix block
+    double* red;
+    double s[RPT];
+    int kmx[RPT];
+    long long off[RPT];
+    int nrows_here;
+
+    __device__ SolveTeam(const StaticDev& S_, const double* sx_, const double* Cd_, double* red_)
+        : S(S_), sx(sx_), Cd(Cd_), red(red_) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int r = threadIdx.x + i * TPD;
+            if (r < S.nrows) {
+                s[i] = row_level(S, sx, r);
+                kmx[i] = S.kmax[r];
+                off[i] = S.off[r];
+            } else {
+                s[i] = 0.0;
+                kmx[i] = 0;
+                off[i] = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ int count(int i, double v, int klo, int khi) const {
+        const double g = (v - s[i]) / S.w0;                     // var_function (Q10)
+        return count_le(sx, g, klo, khi);
+    }
+    __device__ __forceinline__ double pref(int i, int k) const { return k > 0 ? Cd[off[i] + k - 1] : 0.0; }
+    // Full slab (a, b] for this date.
+    __device__ double slab(double a, double b) {
+        double part = 0.0;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            if (kmx[i] == 0) continue;
+            const int ka = count(i, a, 0, kmx[i]);
+            const int kb = count(i, b, 0, kmx[i]);
+            if (kb > ka) part += pref(i, kb) - pref(i, ka);
+        }
+        return TeamReduce<TPD>::sum(part, red);
+    }
+};
+
+// Steps (i)-(iii) of calc_var + K bisection iterations.  Writes snaps[t][0..K]
+// (= (lo+hi)/2 after k updates) and folds iterations-needed / nonzero masks
+// into the rank header.
+template <int TPD, int RPT>
+__global__ __launch_bounds__(TPD) void k_solve_prefix(StaticDev S, SolveConst P, const double* __restrict__ C,
+                                                      double* __restrict__ snaps, Header* hdr) {
+    __shared__ double sx[512];
+    __shared__ double red[TPD / 64 > 0 ? TPD / 64 : 1];
+    for (int j = threadIdx.x; j < S.n; j += TPD) sx[j] = S.x[j];
+    __syncthreads();
+    const long long t = blockIdx.x;
+    SolveTeam<TPD, RPT> tm(S, sx, C + t * S.G, red);
+
+    // (i) r0 = I(lower, first_guess]                            calc_var_class.py:114-121
+    const double r0 = tm.slab(P.lower, P.fg);
+    // (ii) second bracket                                        :125-142
+    const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+    const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+    const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;                          // Q1
+    const double nr = tm.slab(nl, nu);
+    const double F = (nl == P.fg) ? r0 + nr : r0 - nr;                           // adjust_integral
+    // (iii) bracket classification                                :147-160 (Q3 -> NaN)
+    double lo = __builtin_nan(""), hi = __builtin_nan("");
+    if (F > P.obj) { lo = P.vmin; hi = P.sg0; }
+    if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; }
+    if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; }
+    if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; }
+    bool ustack = !(hi == P.sg0 || hi == P.sg1);
+
+    int kLo[RPT], kHi[RPT];
+    double cLo[RPT], cHi[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        kLo[i] = tm.kmx[i] ? tm.count(i, lo, 0, tm.kmx[i]) : 0;
+        kHi[i] = tm.kmx[i] ? tm.count(i, hi, kLo[i], tm.kmx[i]) : 0;
+        cLo[i] = tm.pref(i, kLo[i]);
+        cHi[i] = tm.pref(i, kHi[i]);
+    }
+    // (iv) bisection                                              :250-309
+    double prev = F, prevU = prevU0;
+    int nt = -1;
+    uint64_t mask = 0;
+    double* sn = snaps + t * P.stride;
+    for (int k = 0; k < P.K; ++k) {
+        const double mid = (lo + hi) / 2;
+        if (threadIdx.x == 0) sn[k] = mid;
+        if (nt < 0 && !(hi - lo > P.tol)) nt = k;
+        int kM[RPT];
+        double cM[RPT];
+        double part = 0.0;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            kM[i] = tm.kmx[i] ? tm.count(i, mid, kLo[i], kHi[i]) : 0;
+            cM[i] = tm.pref(i, kM[i]);
+            if (ustack) { if (kM[i] > kLo[i]) part += cM[i] - cLo[i]; }   // slab (lo, mid]
+            else        { if (kHi[i] > kM[i]) part += cHi[i] - cM[i]; }   // slab (mid, hi]
+        }
+        const double val = TeamReduce<TPD>::sum(part, red);
+        const double slab_lower = ustack ? lo : mid;
+        const double Fn = (slab_lower == prevU) ? prev + val : prev - val;     // adjust_integral
+        if (Fn != 0.0) mask |= (1ull << k);                                      // Q4
+        ustack = Fn < P.obj;
+        if (ustack) lo = mid; else hi = mid;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            if (ustack) { kLo[i] = kM[i]; cLo[i] = cM[i]; }
+            else        { kHi[i] = kM[i]; cHi[i] = cM[i]; }
+        }
+        prev = Fn;
+        prevU = mid;
+    }
+    if (threadIdx.x == 0) {
+        sn[P.K] = (lo + hi) / 2;
+        if (nt < 0 && !(hi - lo > P.tol)) nt = P.K;
+        if (nt < 0) atomicOr(&hdr->error, 1);
+        else atomicMax(&hdr->iters, nt);
+        atomicOr((unsigned long long*)&hdr->nonzero, (unsigned long long)mask);
+    }
+}
+
+// Drop-in compute_integral: out[t] = I_t(bounds[t][0], bounds[t][1]].
+template <int TPD, int RPT>
+__global__ __launch_bounds__(TPD) void k_slab_prefix(StaticDev S, const double* __restrict__ C,
+                                                     const double* __restrict__ bounds, double* __restrict__ out) {
+    __shared__ double sx[512];
+    __shared__ double red[TPD / 64 > 0 ? TPD / 64 : 1];
+    for (int j = threadIdx.x; j < S.n; j += TPD) sx[j] = S.x[j];
+    __syncthreads();
+    const long long t = blockIdx.x;
+    SolveTeam<TPD, RPT> tm(S, sx, C + t * S.G, red);
+    const double v = tm.slab(bounds[2 * t], bounds[2 * t + 1]);
+    if (threadIdx.x == 0) out[t] = v;
+}
+
+// Finalise: combine rank headers (Q2 global iteration count, Q4 global break)
+// and pick each date's snapshot; var = mid + ptf_mean (calc_var_class.py:171).
+__global__ void k_finalize(const Header* __restrict__ hdrs, int nranks, const double* __restrict__ snaps,
+                           long long T_total, int stride, int K, double ptf_mean, double* __restrict__ var,
+                           int* __restrict__ err) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    int N = 0, e = 0;
+    unsigned long long nz = 0;
+    for (int r = 0; r < nranks; ++r) {
+        N = max(N, hdrs[r].iters);
+        e |= hdrs[r].error;
+        nz |= hdrs[r].nonzero;
+    }
+    if (N > K) e |= 2;
+    int kstop = min(N, K);
+    for (int k = 0; k < kstop; ++k)
+        if (!((nz >> k) & 1ull)) { kstop = k; break; }
+    if (t == 0) { err[0] = e; err[1] = kstop; err[2] = N; }
+    if (t >= T_total) return;
+    var[t] = snaps[t * stride + kstop] + ptf_mean;
+}
+
+}  // namespace cvq

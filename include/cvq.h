@@ -1,0 +1,168 @@
+/*
+ * cvq.h -- C ABI of the MI355X copula-VaR quadrature engine (libcvq.so).
+ *
+ * Drop-in boundary for the hot path of Nassim-cha/copula-MSM-and-copula-Garch-VaR
+ * (reference @ 2024-11-25).  Each entry point names the reference interface it
+ * replaces.  Plain C: no C++ or torch types, int32 status (0 = ok, < 0 = error,
+ * text in cvq_last_error(), thread-local), caller-owned buffers.
+ *
+ * Memory flags: every buffer argument documented "host|device" is interpreted
+ * according to the call's `mem` argument (CVQ_MEM_HOST: the library copies it
+ * and returns only when the result is back on the host; CVQ_MEM_DEVICE: a
+ * pointer into device memory of the plan's device, used in stream order on the
+ * plan's stream, no host synchronisation).
+ */
+#ifndef CVQ_H
+#define CVQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ----------------------------------------------------------------- status */
+#define CVQ_OK               0
+#define CVQ_ERR_INVALID     -1   /* bad argument (reference: ValueError)            */
+#define CVQ_ERR_UNSUPPORTED -2   /* e.g. Plackett with dim != 2, dim not in {2,3}   */
+#define CVQ_ERR_HIP         -3   /* HIP runtime error                               */
+#define CVQ_ERR_OOM         -4   /* device allocation failed                        */
+#define CVQ_ERR_STATE       -5   /* call order (e.g. solve before set_dates)        */
+#define CVQ_ERR_RANGE       -6   /* a bound above the plan's v_cap                  */
+#define CVQ_ERR_NUMERIC     -7   /* MSM normaliser 0 (calc_prob.py:64), UKF Z<1e-10
+                                    (estimate.py:219), bisection budget exceeded    */
+
+#define CVQ_MEM_HOST   0
+#define CVQ_MEM_DEVICE 1
+
+/* copula kinds: copulas/{gaussian,student,plackett} */
+#define CVQ_GAUSSIAN 0
+#define CVQ_STUDENT  1
+#define CVQ_PLACKETT 2
+/* model kinds: utils/model_estimation/model/{msm,garch,mean_reverting}_estimation.py */
+#define CVQ_MSM   0
+#define CVQ_GARCH 1
+#define CVQ_UKF   2
+
+/* quadrature strategy (both reproduce the reference) */
+#define CVQ_STRATEGY_PREFIX 0    /* materialise per-date row-prefix joint mass, then solve */
+#define CVQ_STRATEGY_DIRECT 1    /* evaluate each slab's nodes inside the solve kernel     */
+
+typedef struct cvq_plan cvq_plan;
+
+/* Static quadrature inputs = the reference's grids_generations_params
+ * (densities, x_values, step_size, vol_combinations) + integrations_params_static
+ * (MSM unique_vol_states) + packed copula params + portfolio weights.
+ * Replaces: msm_estimation.py:123-137 / garch_estimation.py:133-145 outputs as
+ * consumed by calc_integral.py:8-119. */
+typedef struct cvq_static {
+    int32_t model;              /* CVQ_MSM | CVQ_GARCH | CVQ_UKF                        */
+    int32_t copula;             /* CVQ_GAUSSIAN | CVQ_STUDENT | CVQ_PLACKETT            */
+    int32_t dim;                /* assets: 2 or 3                                        */
+    int32_t n;                  /* num_points                                            */
+    int32_t q;                  /* unique vol states per asset (GARCH/UKF: 1)            */
+    int32_t n_combos;           /* q**dim                                                */
+    const double*  x_values;    /* [n]         host                                      */
+    const double*  step;        /* [n]         host                                      */
+    const double*  densities;   /* [dim][q][n] host (GARCH/UKF: ones)                    */
+    const int32_t* combos;      /* [n_combos][dim] host, ij-meshgrid order               */
+    const double*  weights;     /* [dim]       host, weights[0] > 0                      */
+    const double*  vol_states;  /* [dim][q]    host, MSM unique_vol_states; else NULL    */
+    const double*  copula_params; /* packed as copula_integrations_params              */
+    int32_t n_copula_params;    /* Student 1+d(d-1)/2, Gaussian d(d-1)/2, Plackett 1     */
+    int32_t strategy;           /* CVQ_STRATEGY_*                                        */
+    double  v_cap;              /* largest portfolio level any query may use (e.g. 0)    */
+} cvq_static;
+
+/* calc_var arguments: utils/calc_var_class.py:95 (obj_var, first_guess,
+ * second_guess) + the constants of :111-114 and :257. */
+typedef struct cvq_solve_args {
+    double obj_var;             /* 0.05   */
+    double first_guess;         /* -3     */
+    double second_guess_lo;     /* -3.5   */
+    double second_guess_hi;     /* -2     */
+    double min_var;             /* -7.5   */
+    double max_var;             /* 0      */
+    double lower;               /* -100   */
+    double tolerance;           /* 1e-6   */
+    double ptf_mean;            /* load_data.py:113, added at calc_var_class.py:171 */
+} cvq_solve_args;
+
+const char* cvq_last_error(void);
+int32_t     cvq_version(void);
+int32_t     cvq_device_count(int32_t* count);
+
+/* Plan = one device + one stream + device copies of the static tables. */
+int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out);
+int32_t cvq_plan_destroy(cvq_plan* plan);
+/* Run on an external stream (hipStream_t, e.g. torch.cuda.current_stream());
+ * NULL restores the plan's own stream. */
+int32_t cvq_plan_set_stream(cvq_plan* plan, void* hip_stream);
+/* Reachable quadrature nodes per date (nodes with level <= v_cap in the box). */
+int32_t cvq_plan_info(const cvq_plan* plan, int64_t* reach_nodes, int32_t* rows);
+
+/* Per-date inputs = integrations_params_t (calc_integral.py:158):
+ *   MSM:       a = forecasts_by_states [T][dim][q], b = forecasts [T][n_combos]
+ *   GARCH/UKF: a = sigma forecasts [T][dim],        b = NULL                 */
+int32_t cvq_set_dates(cvq_plan* plan, int64_t T, const double* a, const double* b, int32_t mem);
+
+/* Drop-in for ValueAtRiskCalcualtion.compute_integral (calc_var_class.py:179-212)
+ * == calc_grids_and_integrals_results (calc_integral.py:8-119):
+ * out[t] = integral of the joint copula density over the nested grid of
+ * (bounds[t][0], bounds[t][1]] for date t.  bounds [T][2], out [T]. */
+int32_t cvq_slab(cvq_plan* plan, const double* bounds, double* out, int32_t mem);
+
+/* Drop-in for ValueAtRiskCalcualtion.calc_var (calc_var_class.py:95-177 +
+ * bisection_algorithm :250-309), quirks Q1-Q4 reproduced.  var_out [T];
+ * iters_out = bisection iterations the reference would run (may be NULL). */
+int32_t cvq_solve(cvq_plan* plan, const cvq_solve_args* args, double* var_out,
+                  int32_t* iters_out, int32_t mem);
+
+/* Sharded solve, for one process per GPU (date blocks).
+ * Phase 1 (local):  per-date bisection snapshots + a 16-byte header
+ *   d_header: 16 bytes device, d_snaps: [T_local][cvq_snap_stride(args)] device.
+ * Exchange: the caller all-gathers headers and snaps (RCCL).
+ * Phase 2: finalise every date from the gathered blocks; d_var [T_total] device. */
+int32_t cvq_snap_stride(const cvq_solve_args* args, int32_t* stride);
+int32_t cvq_solve_local(cvq_plan* plan, const cvq_solve_args* args, void* d_header, double* d_snaps);
+int32_t cvq_solve_finalize(cvq_plan* plan, const cvq_solve_args* args, const void* d_headers,
+                           int32_t n_ranks, const double* d_snaps, int64_t dates_per_rank,
+                           int64_t T_total, double* d_var);
+
+/* ------------------------------------------------ per-date forecast stage */
+/* MSM forecasts_array (msm_estimation.py:140-202 -> calc_marginals.py:33-38 ->
+ * calc_prob.py:8-69): filtered state probabilities at the end of each rolling
+ * window.  returns_c: centred returns [n_in + T - 1] of ONE asset; out [T][2**k]. */
+int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
+                       const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
+/* GARCH(1,1) compute_forecast (garch_estimation.py:190-231 -> garch/forecast.py:5-19).
+ * out [T] = sigma forecast per window. */
+int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double beta,
+                           const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
+/* UKF compute_forecast (mean_reverting_estimation.py:192-232 -> forecast.py:5-12 ->
+ * estimate.py:230-281); Q19 semantics.  out [T]. */
+int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q,
+                         const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
+
+/* --------------------------------------- batched in-sample likelihoods */
+/* One log-likelihood per parameter candidate over the same return series
+ * (optimiser inner loops).  params: MSM [B][4] = (m0, sigma, b, gamma);
+ * GARCH [B][3] = (omega, alpha, beta); UKF [B][3] = (a, l, q).  out [B].
+ * MSM: calc_prob.py:36-47; GARCH: garch/estimation.py:91-125; UKF: estimate.py:276. */
+int32_t cvq_msm_loglik(int32_t device, int32_t k, const double* params, int64_t B,
+                       const double* returns, int64_t N, double* out, int32_t mem);
+int32_t cvq_garch_loglik(int32_t device, const double* params, int64_t B,
+                         const double* returns, int64_t N, double* out, int32_t mem);
+int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B,
+                       const double* returns, int64_t N, double* out, int32_t mem);
+
+/* Special functions on the device (known-answer tests against scipy):
+ * fn 0 = t.ppf(u, nu) (student.py:102), 1 = norm.ppf (gaussian.py:44),
+ * 2 = erf (utils/utils.py:20). */
+int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int64_t n,
+                    double* out, int32_t mem);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVQ_H */

@@ -219,6 +219,31 @@ def kat_special():
         out[f"tppf_nu{nu:g}"] = stats.t.ppf(u, nu)
     out["tppf_nus"] = np.array([1.0, 2.0, 3.0, 4.5, 5.364, 6.0, 10.0, 30.0, 150.0])
     out["ndtri"] = stats.norm.ppf(u)
+    # mpmath ground truth (scipy's stdtrit is clamped/inaccurate below u ~ 1e-150)
+    import mpmath as mp
+    mp.mp.dps = 40
+    ut = np.concatenate([10.0 ** -np.arange(1, 301, 7.0), [0.3, 0.45, 0.499, 0.7, 0.9, 1 - 1e-9]])
+    out["truth_u"] = ut
+    for nu in (1.0, 3.0, 6.0, 30.0):
+        m_nu = mp.mpf(nu)
+
+        def lower_cdf(s10):                       # F(-10**s10), decreasing in s10
+            t = mp.power(10, s10)
+            return 0.5 * mp.betainc(m_nu / 2, 0.5, 0, m_nu / (m_nu + t * t), regularized=True)
+
+        vals = []
+        for uu in ut:
+            p = mp.mpf(uu) if uu < 0.5 else 1 - mp.mpf(uu)
+            lo, hi = mp.mpf(-20), mp.mpf(330.0 / nu + 10)
+            for _ in range(120):                  # bisection on log10|t|
+                mid = (lo + hi) / 2
+                if lower_cdf(mid) > p:
+                    lo = mid
+                else:
+                    hi = mid
+            tv = -mp.power(10, (lo + hi) / 2)
+            vals.append(float(tv if uu < 0.5 else -tv))
+        out[f"truth_tppf_nu{nu:g}"] = np.array(vals)
     x = np.concatenate([np.linspace(-8, 8, 4001), rng.uniform(-30, 30, 2000), [0.0, -0.0]])
     out["erf_x"] = x
     out["erf"] = special.erf(x)
