@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- VaR dates solved/sec on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 2-asset Student-t copula, MSM(k=4) marginals,
+256x256 nested quadrature grid, 1000 out-of-sample dates per GPU (weak scaling:
+rank r solves dates [r*1000, (r+1)*1000) of one synthetic series; the global
+bisection coupling of the reference (Q2 iteration count, Q4 all-zero break) is
+honoured with ONE all-gather of the per-rank solve headers + bisection snapshots,
+after which every rank finalises the full VaR vector).
+
+One "step" = the calc_var-equivalent scope (utils/calc_var_class.py:95-177) over
+the batch, with the per-date forecast tables already resident in HBM:
+  set per-date inputs (device copy) -> marginal/special-function tables ->
+  joint-mass row prefixes -> per-date bisection solve -> [all-gather] -> finalise.
+
+Prints ONE JSON line (rank 0).  Extra objects:
+  roofline     -- dominant kernel (joint-mass/prefix, k_mass), HIP-event timed
+                  on the plan's stream; algorithmic bytes = 8 B x reachable nodes
+                  x dates per launch.
+  cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
+                  timed on a bounded sample of the same workload, rank 0 at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "copula-msm-and-copula-garch-var_amd")
+sys.path[:0] = [PKG, REPO]
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (vendor figure)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
+    ap.add_argument("--dates-per-gpu", type=int, default=None)
+    ap.add_argument("--strategy", default="prefix", choices=["prefix", "direct"])
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
+    ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
+    ap.add_argument("--cpu-jobs", type=int, default=0)
+    ap.add_argument("--e2e", type=int, default=0, help="also time the device forecast stage")
+    return ap.parse_args()
+
+
+def build_inputs(cfg, T_total, rank, world, device):
+    """Synthetic returns for all dates; this rank's per-date tables via the device filters."""
+    from copula_var import synthetic, tables
+    c = cfg.with_(T=T_total)
+    rets = synthetic.simulate_returns(c)
+    mean, ptf_mean, centred, T = tables.insample_split(rets, c.n_in, c.weights)
+    per = T_total // world
+    lo = rank * per
+    block = centred[lo: lo + c.n_in + per]                       # windows lo .. lo+per-1
+    t0 = time.time()
+    if c.model == "msm":
+        ipt, uvs, ggp = tables.msm_integration_params(block, c.n_in, c.msm_params, c.k, c.num_points, device)
+    else:
+        ipt, uvs, ggp = tables.sigma_integration_params(block, c.n_in, c.model, c.model_params(), c.num_points, device)
+    t_fc = time.time() - t0
+    return c, ipt, uvs, ggp, ptf_mean, per, t_fc, block
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+    from copula_var import engine, synthetic
+    from copula_var import _native as N
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = synthetic.baseline_configs()[a.config]
+    per_gpu = a.dates_per_gpu or cfg.T
+    T_total = per_gpu * world
+    c, ipt, uvs, ggp, ptf_mean, per, t_fc, block = build_inputs(cfg, T_total, rank, world, local)
+    dens, x, step, combos = ggp
+    plan = engine.QuadraturePlan(c.model, c.copula, c.dim, x, step, dens, combos, c.weights,
+                                 c.copula_params(), vol_states=uvs, device=local, strategy=a.strategy)
+    stream = torch.cuda.current_stream()
+    plan.set_stream(stream.cuda_stream)
+    dev = torch.device("cuda", local)
+    if c.model == "msm":
+        d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
+        d_b = torch.tensor(ipt[1], dtype=torch.float64, device=dev).contiguous()
+        b_ptr = d_b.data_ptr()
+    else:
+        d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
+        d_b, b_ptr = None, None
+    args = engine.solve_args(ptf_mean)
+    stride = plan.snap_stride(args)
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)                  # 16-byte header
+    snaps = torch.full((per, stride), float("nan"), dtype=torch.float64, device=dev)
+    var = torch.empty(T_total, dtype=torch.float64, device=dev)
+    if world > 1:
+        hdr_all = torch.zeros(2 * world, dtype=torch.int64, device=dev)
+        snaps_all = torch.empty((T_total, stride), dtype=torch.float64, device=dev)
+
+    def step_fn():
+        plan.set_dates_device(per, d_a.data_ptr(), b_ptr)             # forces tables + mass recompute
+        if world == 1:
+            plan.solve_device(args, var.data_ptr())
+        else:
+            plan.solve_local(args, hdr.data_ptr(), snaps.data_ptr())
+            dist.all_gather_into_tensor(hdr_all, hdr)
+            dist.all_gather_into_tensor(snaps_all, snaps)
+            plan.solve_finalize(args, hdr_all.data_ptr(), world, snaps_all.data_ptr(), per, T_total,
+                                var.data_ptr())
+
+    for _ in range(a.warmup):
+        step_fn()
+    torch.cuda.synchronize()
+    plan.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step_fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = {k: plan.kernel_time(k) for k in ("tables", "mass", "solve", "finalize")}
+    vals = var.cpu().numpy()
+    ms_step = elapsed / a.steps * 1e3
+    value = T_total * a.steps / elapsed
+
+    mass_ms, mass_n = kt["mass"]
+    mass_avg_s = mass_ms / max(mass_n, 1) / 1e3
+    alg_bytes = 8.0 * plan.reach_nodes * per
+    achieved = alg_bytes / mass_avg_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_cfg{a.config}.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("dates_per_launch") == per and pm.get("strategy", "prefix") == a.strategy:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_baseline:
+        cpu = cpu_baseline(c, ipt, uvs, ggp, ptf_mean, vals, a)
+
+    if rank == 0:
+        out = {
+            "metric": "VaR dates solved/sec, 2-asset Student-copula MSM, 256x256 grid, 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "VaR-dates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (MSM returns, seed 20241125; injected in-sample params; fixed copula)",
+            "config": {"workload": f"cfg{a.config}: {c.name}", "model": c.model, "copula": c.copula,
+                       "dim": c.dim, "grid": f"{c.num_points}^{c.dim}", "dates_per_gpu": per,
+                       "global_dates": T_total, "n_in": c.n_in, "parallelism": f"dates/dp{world}",
+                       "strategy": a.strategy},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_mass (joint-mass row-prefix)", "alg_bytes_per_launch": alg_bytes,
+                         "avg_launch_us": mass_avg_s * 1e6, "reach_nodes_per_date": plan.reach_nodes},
+            "kernels": kernels,
+            "forecast_stage_s": t_fc,
+            "var_checksum": float(np.nansum(vals)),
+            "var_nan": int(np.isnan(vals).sum()),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(c, ipt, uvs, ggp, ptf_mean, gpu_var, a):
+    """joblib CPU path on a bounded sample (first S dates of this workload)."""
+    from oracle import quadrature as Q
+    from oracle.joblib_port import JoblibPath
+    jobs = a.cpu_jobs or min(16, os.cpu_count() or 1)
+    S = a.cpu_dates or jobs
+    dens, x, step, combos = ggp
+    if c.model == "msm":
+        per = (ipt[0][:S], ipt[1][:S])
+    else:
+        per = ipt[0][:S]
+    P = Q.Problem(c.model, c.copula, c.dim, x, step, dens, combos, c.weights, c.copula_params(), per, uvs)
+    J = JoblibPath(P, n_jobs=jobs)
+    t0 = time.perf_counter()
+    var, it, _ = J.calc_var(ptf_mean)
+    wall = time.perf_counter() - t0
+    # the sample's own global iteration count can differ from the full batch's (Q2)
+    return {"value": S / wall, "unit": "VaR-dates/s", "cores": jobs, "kind": "port",
+            "sample": f"first {S} dates of the same workload, full calc_var control flow "
+                      f"({it} bisection iterations), joblib n_jobs={jobs}, scalar t.ppf; wall {wall:.1f}s",
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

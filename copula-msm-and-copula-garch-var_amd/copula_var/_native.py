@@ -72,6 +72,8 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_plan_destroy": (i32, [v]),
         "cvq_plan_set_stream": (i32, [v, v]),
         "cvq_plan_info": (i32, [v, C.POINTER(i64), _ip]),
+        "cvq_plan_timing": (i32, [v, i32]),
+        "cvq_plan_kernel_time": (i32, [v, i32, C.POINTER(d), _ip]),
         "cvq_set_dates": (i32, [v, i64, v, v, i32]),
         "cvq_slab": (i32, [v, v, v, i32]),
         "cvq_solve": (i32, [v, C.POINTER(CvqSolveArgs), v, _ip, i32]),

@@ -86,6 +86,19 @@ class QuadraturePlan:
     def set_stream(self, stream_handle: Optional[int]) -> None:
         N.check(N.lib().cvq_plan_set_stream(self._h, C.c_void_p(stream_handle or 0)), "cvq_plan_set_stream")
 
+    KERNELS = {"tables": 0, "mass": 1, "solve": 2, "finalize": 3, "slab": 4}
+
+    def enable_timing(self, on: bool = True) -> None:
+        """Record HIP events around every kernel launch on the plan's stream."""
+        N.check(N.lib().cvq_plan_timing(self._h, int(bool(on))), "cvq_plan_timing")
+
+    def kernel_time(self, kind: str) -> Tuple[float, int]:
+        """(total milliseconds, launches) of one kernel kind since enable_timing()."""
+        ms, n = C.c_double(), C.c_int32()
+        N.check(N.lib().cvq_plan_kernel_time(self._h, self.KERNELS[kind], C.byref(ms), C.byref(n)),
+                "cvq_plan_kernel_time")
+        return float(ms.value), int(n.value)
+
     # ------------------------------------------------------------ per-date inputs
     def set_dates(self, integrations_params_t) -> None:
         """integrations_params_t as the reference builds it: MSM (forecasts_by_states

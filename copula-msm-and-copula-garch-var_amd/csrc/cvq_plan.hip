@@ -49,7 +49,30 @@ struct cvq_plan {
     int* d_err = nullptr;
     long long capIO = 0;
     double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
+    // optional per-kernel timing (HIP events on the plan's stream)
+    bool timing = false;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> events;
 };
+
+namespace {
+enum TimedKernel { TK_TABLES = 0, TK_MASS = 1, TK_SOLVE = 2, TK_FINALIZE = 3, TK_SLAB = 4, TK_COUNT = 5 };
+
+struct TimedScope {
+    cvq_plan* p;
+    int kind;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedScope(cvq_plan* p_, int kind_) : p(p_), kind(kind_) {
+        if (!p->timing) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+        (void)hipEventRecord(a, p->stream);
+    }
+    ~TimedScope() {
+        if (!a) return;
+        (void)hipEventRecord(b, p->stream);
+        p->events.push_back({kind, {a, b}});
+    }
+};
+}  // namespace
 
 namespace {
 
@@ -128,6 +151,7 @@ void launch_slab_t(cvq_plan* p, const double* bounds, double* out) {
 }
 
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
+    TimedScope ts(p, TK_SOLVE);
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
                 "prefix solve supports at most 4096 rows (3-D n <= 64)");
@@ -142,6 +166,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 }
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
+    TimedScope ts(p, TK_SLAB);
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
                 "prefix slab supports at most 4096 rows (3-D n <= 64)");
@@ -202,12 +227,14 @@ int ensure_mass(cvq_plan* p) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
     if (!p->tables_valid) {
+        TimedScope ts(p, TK_TABLES);
         int rc = dispatch_cop(p, true);
         if (rc) return rc;
         p->tables_valid = true;
         p->mass_valid = false;
     }
     if (!p->mass_valid) {
+        TimedScope ts(p, TK_MASS);
         int rc = dispatch_cop(p, false);
         if (rc) return rc;
         p->mass_valid = true;
@@ -449,6 +476,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     if (!p) return CVQ_OK;
     (void)hipSetDevice(p->device);
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
+    for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io})
@@ -471,6 +499,32 @@ int32_t cvq_plan_info(const cvq_plan* p, int64_t* reach, int32_t* rows) {
     return CVQ_OK;
 }
 
+int32_t cvq_plan_timing(cvq_plan* p, int32_t enable) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
+    p->events.clear();
+    p->timing = enable != 0;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_t* launches) {
+    CVQ_REQUIRE(p != nullptr && total_ms != nullptr && launches != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(kind >= 0 && kind < TK_COUNT, CVQ_ERR_INVALID, "unknown kernel kind");
+    double tot = 0.0;
+    int cnt = 0;
+    for (auto& e : p->events) {
+        if (e.first != kind) continue;
+        CVQ_HIP_CHECK(hipEventSynchronize(e.second.second));
+        float ms = 0.f;
+        CVQ_HIP_CHECK(hipEventElapsedTime(&ms, e.second.first, e.second.second));
+        tot += ms;
+        ++cnt;
+    }
+    *total_ms = tot;
+    *launches = cnt;
+    return CVQ_OK;
+}
+
 int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && a != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(T > 0, CVQ_ERR_INVALID, "T must be > 0");
@@ -479,7 +533,8 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
     const StaticDev& S = p->S;
     const size_t na = (size_t)T * S.dim * (S.model == CVQ_MSM ? S.q : 1);
     const size_t npi = (size_t)T * S.Q;
-    if (T > p->capT) {
+    const bool realloc = T > p->capT;
+    if (realloc) {
         int rc;
         if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi)) ||
             (rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)) ||
@@ -492,9 +547,10 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_a, a, na * sizeof(double), kind, p->stream));
     if (S.model == CVQ_MSM) {
         CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, b, npi * sizeof(double), kind, p->stream));
-    } else {
-        std::vector<double> ones(npi, 1.0);
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), npi * sizeof(double), hipMemcpyHostToDevice, p->stream));
+    } else if (realloc) {                         // GARCH/UKF: pi_t = [1.0] (Q = 1), set once
+        std::vector<double> ones((size_t)p->capT * S.Q, 1.0);
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice,
+                                     p->stream));
         CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     }
     if (mem != CVQ_MEM_DEVICE) CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
@@ -552,6 +608,7 @@ int32_t cvq_solve_finalize(cvq_plan* p, const cvq_solve_args* a, const void* d_h
     if (rc) return rc;
     CVQ_HIP_CHECK(hipSetDevice(p->device));
     const unsigned blocks = (unsigned)std::max<long long>(1, (T_total + 255) / 256);
+    TimedScope ts(p, TK_FINALIZE);
     hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)d_headers, n_ranks,
                        d_snaps, (long long)T_total, stride, stride - 1, a->ptf_mean, d_var, p->d_err);
     CVQ_HIP_CHECK(hipGetLastError());
@@ -578,6 +635,7 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
         CVQ_HIP_CHECK(hipMemsetAsync(p->d_hdr, 0, sizeof(Header), p->stream));
         if ((rc = launch_solve(p, solve_const(*a, K), p->d_snap, p->d_hdr))) return rc;
         const unsigned blocks = (unsigned)((p->T + 255) / 256);
+        TimedScope ts(p, TK_FINALIZE);
         hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)p->d_hdr, 1,
                            (const double*)p->d_snap, p->T, stride, K, a->ptf_mean, d_var, p->d_err);
         CVQ_HIP_CHECK(hipGetLastError());

@@ -101,6 +101,12 @@ int32_t cvq_plan_set_stream(cvq_plan* plan, void* hip_stream);
 /* Reachable quadrature nodes per date (nodes with level <= v_cap in the box). */
 int32_t cvq_plan_info(const cvq_plan* plan, int64_t* reach_nodes, int32_t* rows);
 
+/* Per-kernel timing with HIP events recorded on the plan's stream (bench.py's
+ * live roofline).  kind: 0 tables, 1 joint-mass/prefix, 2 solve, 3 finalize,
+ * 4 slab.  cvq_plan_timing(enable) also clears previous records. */
+int32_t cvq_plan_timing(cvq_plan* plan, int32_t enable);
+int32_t cvq_plan_kernel_time(cvq_plan* plan, int32_t kind, double* total_ms, int32_t* launches);
+
 /* Per-date inputs = integrations_params_t (calc_integral.py:158):
  *   MSM:       a = forecasts_by_states [T][dim][q], b = forecasts [T][n_combos]
  *   GARCH/UKF: a = sigma forecasts [T][dim],        b = NULL                 */
