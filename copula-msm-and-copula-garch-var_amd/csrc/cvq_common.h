@@ -51,6 +51,12 @@ struct alignas(16) Header {       // per-rank solve summary, all-gathered across
 // --------------------------------------------------------------- host errors
 namespace cvq {
 void set_error(const std::string& msg);
+
+constexpr int kCfTerms = 400;     // continued-fraction coefficient table length
+
+// Student-t constants for one nu + device copies of the two CF coefficient tables
+// (written to *d_cf, 2 * kCfTerms doubles, owned by the caller).
+int make_tconst(double nu, TConst* tk, double** d_cf);
 }
 
 #define CVQ_HIP_CHECK(expr)                                                        \

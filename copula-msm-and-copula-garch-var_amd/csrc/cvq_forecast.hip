@@ -507,15 +507,10 @@ int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int6
     int rc = check_device(device);
     if (rc) return rc;
     TConst tk{};
+    DevBuf cf;
     if (fn == 0) {
         CVQ_REQUIRE(nu > 0, CVQ_ERR_INVALID, "nu must be > 0");
-        tk.nu = nu;
-        tk.a = nu / 2;
-        tk.ln_nu = std::log(nu);
-        tk.lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
-        tk.ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
-        tk.ln_tail = tk.ln_k + (nu - 1) / 2 * tk.ln_nu - tk.ln_nu;
-        tk.split = (tk.a + 1.0) / (tk.a + 2.5);
+        if ((rc = make_tconst(nu, &tk, &cf.p))) return rc;
     }
     DevBuf xin, dout;
     const double* d_x;

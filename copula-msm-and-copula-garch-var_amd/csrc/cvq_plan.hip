@@ -16,6 +16,25 @@ namespace cvq {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+int make_tconst(double nu, TConst* tk, double** d_cf) {
+    tk->nu = nu;
+    tk->a = nu / 2;
+    tk->ln_nu = std::log(nu);
+    tk->lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
+    tk->ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
+    tk->ln_tail = tk->ln_k + (nu - 1) / 2 * tk->ln_nu - tk->ln_nu;
+    tk->split = (tk->a + 1.0) / (tk->a + 2.5);
+    std::vector<double> c(2 * kCfTerms);
+    ibeta_cf_coeffs(tk->a, 0.5, c.data(), kCfTerms);
+    ibeta_cf_coeffs(0.5, tk->a, c.data() + kCfTerms, kCfTerms);
+    CVQ_HIP_CHECK(hipMalloc((void**)d_cf, c.size() * sizeof(double)));
+    CVQ_HIP_CHECK(hipMemcpy(*d_cf, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    tk->cf_dir = *d_cf;
+    tk->cf_cmp = *d_cf + kCfTerms;
+    tk->cf_terms = kCfTerms;
+    return CVQ_OK;
+}
+
 }  // namespace cvq
 
 using namespace cvq;
@@ -32,6 +51,7 @@ struct cvq_plan {
     double* d_F = nullptr;
     double* d_phi = nullptr;
     double* d_uvs = nullptr;
+    double* d_cf = nullptr;      // Student-t CF coefficient tables
     int* d_kmax = nullptr;
     long long* d_off = nullptr;
     // per-date state
@@ -188,15 +208,29 @@ void launch_tables_t(cvq_plan* p) {
                        p->d_tB);
 }
 
-size_t mass_lds_bytes(const StaticDev& S) {
-    return sizeof(double) * (4 * (size_t)S.n + 2 * (size_t)S.q * S.n + 2 * (size_t)S.q * S.q + S.Q);
+template <int COP, bool MSM, int DIM, int QT>
+void launch_mass_q(cvq_plan* p) {
+    const dim3 grid((unsigned)p->T, (unsigned)((p->S.nrows + 63) / 64));
+    hipLaunchKernelGGL((k_mass<COP, MSM, DIM, QT>), grid, dim3(64), 0, p->stream, p->S, p->d_tA, p->d_tB, p->d_pi,
+                       p->d_C);
 }
 
 template <int COP, bool MSM, int DIM>
 void launch_mass_t(cvq_plan* p) {
-    const dim3 grid((unsigned)p->T, DIM == 3 ? (unsigned)p->S.n : 1u);
-    hipLaunchKernelGGL((k_mass<COP, MSM, DIM>), grid, dim3(256), mass_lds_bytes(p->S), p->stream, p->S, p->d_tA,
-                       p->d_tB, p->d_pi, p->d_C);
+    if constexpr (!MSM) {
+        launch_mass_q<COP, false, DIM, 1>(p);
+    } else {
+        switch (p->S.q) {
+            case 1: launch_mass_q<COP, true, DIM, 1>(p); break;
+            case 2: launch_mass_q<COP, true, DIM, 2>(p); break;
+            case 3: launch_mass_q<COP, true, DIM, 3>(p); break;
+            case 4: launch_mass_q<COP, true, DIM, 4>(p); break;
+            case 5: launch_mass_q<COP, true, DIM, 5>(p); break;
+            case 6: launch_mass_q<COP, true, DIM, 6>(p); break;
+            case 7: launch_mass_q<COP, true, DIM, 7>(p); break;
+            default: launch_mass_q<COP, true, DIM, 8>(p); break;
+        }
+    }
 }
 
 template <int COP>
@@ -394,14 +428,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
             S.uni_ex = -(nu + 1) / 2;
             const double m2 = -2.0 * S.node_ex;
             S.node_m = (m2 == std::floor(m2) && m2 <= 128.0) ? (int)m2 : -1;
-            TConst& tk = S.tk;
-            tk.nu = nu;
-            tk.a = nu / 2;
-            tk.ln_nu = std::log(nu);
-            tk.lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
-            tk.ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
-            tk.ln_tail = tk.ln_k + (nu - 1) / 2 * tk.ln_nu - tk.ln_nu;
-            tk.split = (tk.a + 1.0) / (tk.a + 2.5);
+            if (int rc2 = make_tconst(nu, &S.tk, &p->d_cf)) { cvq_plan_destroy(p); return rc2; }
         } else {
             S.term1 = 1 / (std::sqrt(std::pow(2 * M_PI, d) * det));                              // gaussian.py:107
         }
@@ -467,7 +494,6 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
         S.phi = p->d_phi;
     }
-    CVQ_REQUIRE(mass_lds_bytes(S) <= 64 * 1024, CVQ_ERR_UNSUPPORTED, "quadrature tables exceed 64 KiB of LDS");
     *out = p;
     return CVQ_OK;
 }
@@ -477,7 +503,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     (void)hipSetDevice(p->device);
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
-    for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_kmax,
+    for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io})
         if (b) (void)hipFree(b);

@@ -109,20 +109,21 @@ __device__ __forceinline__ double node_value(const StaticDev& S, const RowCtx& r
         c = (num / den) * (r.B * Bc);
     } else {
         double qf;
+        // z^T R^-1 z in the order of student.py:136 (rounding differences ~1e-16)
         if (DIM == 2) {
-            const double y0 = r.p0 + zc * S.Ri[2];
-            const double y1 = r.p1 + zc * S.Ri[3];
-            qf = y0 * r.z0 + y1 * zc;
+            const double y0 = fma(zc, S.Ri[2], r.p0);
+            const double y1 = fma(zc, S.Ri[3], r.p1);
+            qf = fma(y1, zc, y0 * r.z0);
         } else {
-            const double y0 = r.p0 + zc * S.Ri[6];
-            const double y1 = r.p1 + zc * S.Ri[7];
-            const double y2 = r.p2 + zc * S.Ri[8];
-            qf = (y0 * r.z0 + y1 * r.z1) + y2 * zc;
+            const double y0 = fma(zc, S.Ri[6], r.p0);
+            const double y1 = fma(zc, S.Ri[7], r.p1);
+            const double y2 = fma(zc, S.Ri[8], r.p2);
+            qf = fma(y2, zc, fma(y1, r.z1, y0 * r.z0));
         }
         double mv;
         if (COP == CVQ_STUDENT) {
             const bool fin = r.fin && isfinite(zc);
-            mv = fin ? S.term1 * pow_node(1.0 + qf * S.inv_nu, S.node_m, S.node_ex) : 0.0;   // :133-141
+            mv = fin ? S.term1 * pow_node(fma(qf, S.inv_nu, 1.0), S.node_m, S.node_ex) : 0.0;   // :133-141
         } else {
             mv = S.term1 * exp(-0.5 * qf);                         // gaussian.py:105-113
         }
@@ -155,118 +156,109 @@ __device__ __forceinline__ RowCtx make_row(const StaticDev& S, double z0, double
     return r;
 }
 
-// ------------------------------------------------- MSM / Delta-product weights
-// W(node) = sum_l pi_t[l] Delta[node, l]  with  Delta = prod_c F_c(combo_c, i_c)
-// (create_grids.py:121,143; Q5 rotation baked into F; Q6: in 3-D the axis-0
-// factor only where i1 == 0).  Contracted as G_row[b] (outer axes) . F_inner(b, col).
-// LDS block used by k_mass / k_solve_direct:
-struct WeightsLds {
-    double* cF;   // [q][n]  inner-axis F
-    double* rG;   // [n][q]  per outer row (2-D: i0; 3-D: i1 with fixed i0)
-    double* H;    // 3-D: [2][q][q]
-    double* pi;   // [Q]
-};
-
-// Fill rG for the n outer rows of this block.  2-D: rows are i0.  3-D: block i0, rows i1.
-__device__ inline void build_row_weights(const StaticDev& S, const WeightsLds& L, int i0_block, int dim) {
-    const int n = S.n, q = S.q;
-    if (dim == 3) {
-        for (int bc = threadIdx.x; bc < q * q; bc += blockDim.x) {
-            double hw = 0.0, ho = 0.0;
-            for (int a = 0; a < q; ++a) {
-                const double p = L.pi[a * q * q + bc];
-                hw += p * S.F[(size_t)a * n + i0_block];         // axis-0 factor F_0(a, i0)
-                ho += p;                                         // axis-0 factor reset to 1 (Q6)
-            }
-            L.H[bc] = hw;
-            L.H[q * q + bc] = ho;
-        }
-        __syncthreads();
-    }
-    for (int rb = threadIdx.x; rb < n * q; rb += blockDim.x) {
-        const int r = rb / q, b = rb % q;
-        double g = 0.0;
-        if (dim == 2) {
-            for (int a = 0; a < q; ++a) g += L.pi[a * q + b] * S.F[(size_t)a * n + r];
-        } else {
-            const double* H = L.H + (r == 0 ? 0 : q * q);
-            for (int bb = 0; bb < q; ++bb) g += H[bb * q + b] * S.F[((size_t)q + bb) * n + r];
-        }
-        L.rG[rb] = g;
-    }
-}
-
 // ------------------------------------------------------------------ k_mass
 // PREFIX strategy: C[t][off[r] + j - 1] = sum_{j' <= j} node(t, r, j') for every
-// reachable node (level <= v_cap).  grid = (T, dim == 3 ? n : 1), 256 threads,
-// one wavefront per row, 64 columns per step, inclusive scan in registers.
-template <int COP, bool MSM, int DIM>
-__global__ __launch_bounds__(256) void k_mass(StaticDev S, const double* __restrict__ tA,
-                                              const double* __restrict__ tB, const double* __restrict__ pi,
-                                              double* __restrict__ C) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    constexpr int QM = MSM ? kMaxQ : 1;
-    const int n = S.n, q = S.q;
+// reachable node (level <= v_cap) of date t.
+//
+// Mapping: one 64-lane wavefront per (date, group of 64 rows); lane = row.
+// All lanes walk the inner (column) axis together, so every column-table
+// operand is wave-uniform (scalar loads, SGPR operands) and each lane keeps its
+// row's running prefix in a register -- no cross-lane scan.  Blocks of 16
+// columns are transposed through LDS so the global stores are 4 rows x 128 B
+// contiguous per instruction.
+//
+// W(node) = sum_l pi_t[l] Delta[node, l], Delta = prod_c F_c(combo_c, i_c)
+// (create_grids.py:121,143; Q5 rotation baked into F; Q6: in 3-D the axis-0
+// factor only where i1 == 0), contracted per row as G[b] and per column as F_inner(b, j).
+template <int COP, bool MSM, int DIM, int QT>
+__global__ __launch_bounds__(64) void k_mass(StaticDev S, const double* __restrict__ tA,
+                                             const double* __restrict__ tB, const double* __restrict__ pi,
+                                             double* __restrict__ C) {
+    constexpr int CB = 16;                       // columns per transpose block
+    constexpr int LD = CB + 1;                   // padded LDS row (conflict-free b64 access)
+    __shared__ double tile[64 * LD];
+    const int lane = threadIdx.x;
     const long long t = blockIdx.x;
-    const int blk = blockIdx.y;
-    double* cA = lds;
-    double* cB = cA + n;
-    double* rA = cB + n;
-    double* rB = rA + n;
-    WeightsLds L;
-    L.cF = rB + n;
-    L.rG = L.cF + (size_t)q * n;
-    L.H = L.rG + (size_t)q * n;
-    L.pi = L.H + 2 * q * q;
-    const int inner = DIM - 1, rowaxis = DIM - 2;
+    const int n = S.n, q = QT;
+    const int r = blockIdx.y * 64 + lane;
+    const bool live = r < S.nrows;
     const double* At = tA + t * S.dim * n;
     const double* Bt = tB + t * S.dim * n;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        cA[j] = At[inner * n + j];
-        cB[j] = Bt[inner * n + j];
-        rA[j] = At[rowaxis * n + j];
-        rB[j] = Bt[rowaxis * n + j];
-        for (int b = 0; b < q; ++b) L.cF[b * n + j] = S.F[((size_t)inner * q + b) * n + j];
-    }
-    for (int l = threadIdx.x; l < S.Q; l += blockDim.x) L.pi[l] = pi[t * S.Q + l];
-    __syncthreads();
-    build_row_weights(S, L, blk, DIM);
-    __syncthreads();
+    const double* pit = pi + t * S.Q;
+    const int inner = DIM - 1;
+    const double* Ac = At + inner * n;           // inner-axis tables (wave-uniform reads)
+    const double* Bc = Bt + inner * n;
+    const double* Fc = S.F + (size_t)inner * q * n;
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const double z0fix = (DIM == 3) ? At[blk] : 0.0;
-    const double B0fix = (DIM == 3) ? Bt[blk] : 1.0;
-    double* Cd = C + t * S.G;
-    for (int rl = wave; rl < n; rl += nw) {
-        const int r = (DIM == 2) ? rl : blk * n + rl;
-        const int km = S.kmax[r];
-        if (km == 0) continue;
-        double* Cr = Cd + S.off[r];
-        const RowCtx ctx = (DIM == 2) ? make_row<COP, DIM>(S, rA[rl], 0.0, rB[rl])
-                                      : make_row<COP, DIM>(S, z0fix, rA[rl], B0fix * rB[rl]);
-        double G[QM];
+    const int rr_ = live ? r : 0;
+    const int i0 = (DIM == 2) ? rr_ : rr_ / n;
+    const int i1 = (DIM == 2) ? 0 : rr_ % n;
+
+    // ---- row weights G[b] (outer axes contracted with pi_t)
+    double G[QT];
+    if (DIM == 2) {
 #pragma unroll
-        for (int b = 0; b < QM; ++b) G[b] = (b < q) ? L.rG[rl * q + b] : 0.0;
-        double carry = 0.0;
-        for (int j0 = 1; j0 <= km; j0 += 64) {
-            const int j = j0 + lane;
-            double v = 0.0;
-            if (j <= km) {
+        for (int b = 0; b < QT; ++b) {
+            double g = 0.0;
+#pragma unroll
+            for (int a = 0; a < QT; ++a) g = fma(pit[a * q + b], S.F[(size_t)a * n + i0], g);
+            G[b] = g;
+        }
+    } else {
+        double f0[QT], f1[QT];
+#pragma unroll
+        for (int a = 0; a < QT; ++a) {
+            f0[a] = (i1 == 0) ? S.F[(size_t)a * n + i0] : 1.0;     // Q6: axis-0 factor only at i1 == 0
+            f1[a] = S.F[((size_t)q + a) * n + i1];
+        }
+#pragma unroll
+        for (int c = 0; c < QT; ++c) {
+            double g = 0.0;
+#pragma unroll
+            for (int b = 0; b < QT; ++b) {
+                double h = 0.0;
+#pragma unroll
+                for (int a = 0; a < QT; ++a) h = fma(pit[(a * q + b) * q + c], f0[a], h);
+                g = fma(h, f1[b], g);
+            }
+            G[c] = g;
+        }
+    }
+    // ---- row context
+    RowCtx ctx;
+    if (DIM == 2) ctx = make_row<COP, DIM>(S, At[i0], 0.0, Bt[i0]);
+    else ctx = make_row<COP, DIM>(S, At[i0], At[n + i1], Bt[i0] * Bt[n + i1]);   // prod over axes in order
+    const int km = live ? S.kmax[r] : 0;
+    const long long off = live ? S.off[r] : 0;
+    int maxlen = km;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, o, 64));
+    double* Cd = C + t * S.G;
+
+    double acc = 0.0;
+    for (int jb = 1; jb <= maxlen; jb += CB) {
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int j = jb + c;                 // wave-uniform
+            if (j < n) {
                 double W = 0.0;
 #pragma unroll
-                for (int b = 0; b < QM; ++b)
-                    if (b < q) W += G[b] * L.cF[b * n + j];
-                v = node_value<COP, MSM, DIM>(S, ctx, cA[j], cB[j], W);
+                for (int b = 0; b < QT; ++b) W = fma(G[b], Fc[(size_t)b * n + j], W);
+                const double v = node_value<COP, MSM, DIM>(S, ctx, Ac[j], Bc[j], W);
+                if (j <= km) acc += v;
             }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const double y = __shfl_up(v, o, 64);
-                if (lane >= o) v += y;
-            }
-            v += carry;
-            if (j <= km) Cr[j - 1] = v;
-            carry = __shfl(v, 63, 64);
+            tile[lane * LD + c] = acc;
         }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+        for (int rr = 0; rr < 64; rr += 4) {
+            const int row = rr + (lane >> 4), col = lane & 15;
+            const int krow = __shfl(km, row, 64);
+            const long long orow = __shfl(off, row, 64);
+            const int j = jb + col;
+            if (j <= krow) Cd[orow + j - 1] = tile[row * LD + col];
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 

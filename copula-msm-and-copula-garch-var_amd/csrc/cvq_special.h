@@ -23,35 +23,43 @@ struct TConst {
     double ln_k;        // log of Gamma((nu+1)/2) / (sqrt(nu pi) Gamma(nu/2))
     double ln_tail;     // log(k_nu) + (nu-1)/2 log(nu) - log(nu): F(t) ~ exp(ln_tail) |t|^-nu
     double split;       // (a + 1) / (a + 1/2 + 2): continued-fraction branch point
+    const double* cf_dir;   // CF coefficients c_k of I_x(a, 1/2)   (d_k = c_k x), device
+    const double* cf_cmp;   // CF coefficients c_k of I_y(1/2, a),  device
+    int cf_terms;           // table length
 };
+
+// Host: continued-fraction coefficients of the regularised incomplete beta
+// I_x(a, b) = x^a (1-x)^b / (a B(a,b)) * 1/(1 + d1/(1 + d2/(1 + ...))), d_k = c_k x:
+//   c_{2m+1} = -(a+m)(a+b+m) / ((a+2m)(a+2m+1)),   c_{2m} = m(b-m) / ((a+2m-1)(a+2m)).
+inline void ibeta_cf_coeffs(double a, double b, double* c, int terms) {
+    for (int k = 1; k <= terms; ++k) {
+        const int m = k / 2;
+        if (k & 1) c[k - 1] = -(a + m) * (a + b + m) / ((a + 2.0 * m) * (a + 2.0 * m + 1.0));
+        else c[k - 1] = m * (b - m) / ((a + 2.0 * m - 1.0) * (a + 2.0 * m));
+    }
+}
 
 __device__ __forceinline__ double pos_inf() { return __builtin_huge_val(); }
 
-// Continued fraction of the regularised incomplete beta, modified Lentz.
-__device__ inline double ibeta_cf(double a, double b, double x) {
-    const double tiny = 1e-300, eps = 2.0e-16;
-    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
-    double c = 1.0;
-    double d = 1.0 - qab * x / qap;
-    if (fabs(d) < tiny) d = tiny;
-    d = 1.0 / d;
-    double h = d;
-    for (int m = 1; m <= 400; ++m) {
-        const double m2 = 2.0 * m;
-        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
-        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        h *= d * c;
-        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
-        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < eps) break;
+// 1/(1 + d1/(1 + d2/(1 + ...))), d_k = c[k-1] x, by the forward recurrence of
+// the convergents A_k / B_k (no division per term; the coefficient index is
+// wave-uniform, so c[] comes through the scalar cache).
+__device__ inline double ibeta_cf(const double* __restrict__ c, int terms, double x) {
+    double Am = 1.0, Bm = 1.0;      // A_1, B_1
+    double Ap = 0.0, Bp = 1.0;      // A_0, B_0
+    for (int k = 1; k < terms; k += 2) {
+        double An = fma(c[k - 1] * x, Ap, Am), Bn = fma(c[k - 1] * x, Bp, Bm);
+        Ap = Am; Bp = Bm; Am = An; Bm = Bn;
+        An = fma(c[k] * x, Ap, Am); Bn = fma(c[k] * x, Bp, Bm);
+        Ap = Am; Bp = Bm; Am = An; Bm = Bn;
+        // |A_k/B_k - A_{k-1}/B_{k-1}| <= 1e-16 |A_k/B_k|
+        if (fabs(fma(Am, Bp, -Ap * Bm)) <= 1e-16 * fabs(Am * Bp)) break;
+        if (fabs(Bm) > 1e150) {
+            const double s = 1.0 / Bm;
+            Am *= s; Ap *= s; Bp *= s; Bm = 1.0;
+        }
     }
-    return h;
+    return Am / Bm;
 }
 
 // log F_nu(t) and log pdf_nu(t) for t <= 0.
@@ -75,12 +83,12 @@ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, doub
         // F = 0.5 * I_x(a, 1/2) = 0.5 * x^a (1-x)^(1/2) / (a B) * cf
         const double ln1mx = ln_t2 - L;
         *lnF = -0.69314718055994530942 + k.a * lnx + 0.5 * ln1mx - k.lbeta - log(k.a) +
-               log(ibeta_cf(k.a, 0.5, x));
+               log(ibeta_cf(k.cf_dir, k.cf_terms, x));
     } else {
         // F = 0.5 * (1 - I_y(1/2, a)),  y = t^2 / (nu + t^2) small
         const double y = (at * at) / (k.nu + at * at);
         double front = 0.0;
-        if (y > 0.0) front = exp(0.5 * log(y) + k.a * log1p(-y) - k.lbeta) / 0.5 * ibeta_cf(0.5, k.a, y);
+        if (y > 0.0) front = exp(0.5 * log(y) + k.a * log1p(-y) - k.lbeta) * 2.0 * ibeta_cf(k.cf_cmp, k.cf_terms, y);
         *lnF = log(0.5 * (1.0 - front));
     }
 }
@@ -132,39 +140,59 @@ __device__ inline double stdtrit(const TConst& k, double p) {
     double tcf = z + (z2 * z + z) / (4.0 * nu) +
                  (((5.0 * z2 + 16.0) * z2 + 3.0) * z) / (96.0 * nu * nu) +
                  ((((3.0 * z2 + 19.0) * z2 + 17.0) * z2 - 15.0) * z) / (384.0 * nu * nu * nu);
-    const double ttail = -exp((k.ln_tail - log(pp)) / nu);
+    // power tail F ~ exp(ln_tail)|t|^-nu (1 - nu^2 (nu+1) / (2 (nu+2) t^2)), two terms
+    double ttail = -exp((k.ln_tail - log(pp)) / nu);
+    ttail *= 1.0 - nu * (nu + 1.0) / (2.0 * (nu + 2.0) * ttail * ttail);
     t = (ttail < tcf && z2 > nu) ? ttail : tcf;
     if (nu > 1e5) return upper ? -tcf : tcf;
     if (!(t < 0.0)) t = -1e-3;
     const double lp = log(pp);
     double lo = -pos_inf(), hi = 0.0;          // F(lo) < pp < F(hi)
-    for (int it = 0; it < 100; ++it) {
+    // Halley on g(t) = log F(t) - log pp (cubic convergence; stop once a step is
+    // below 1e-6 relative: the next error is then ~1e-18).
+    for (int it = 0; it < 60; ++it) {
         double lnF, lpdf;
         t_lower_logs(k, t, &lnF, &lpdf);
         const double g = lnF - lp;
         if (g > 0.0) hi = t; else lo = t;
         if (g == 0.0) break;
-        const double step = g / exp(lpdf - lnF);   // g / (pdf / F)
-        double tn = t - step;
-        if (!(tn > lo && tn < hi)) {
+        const double h = exp(lpdf - lnF);                   // g'  = pdf / F
+        const double dl = -(nu + 1.0) * t / (nu + t * t);    // pdf'/pdf
+        const double gn = g / h;
+        const double den = 1.0 - 0.5 * gn * (dl - h);       // 1 - g g'' / (2 g'^2)
+        double tn = (den > 0.5 && den < 2.0) ? t - gn / den : t - gn;
+        if (tn == t) break;                                  // correction below one ulp
+        bool fallback = false;
+        if (!(tn >= lo && tn <= hi)) {                        // outside the bracket: bisect
+            fallback = true;
             if (lo == -pos_inf()) tn = 2.0 * t - 1.0;
             else tn = 0.5 * (lo + hi);
         }
-        if (fabs(tn - t) <= 2e-16 * fabs(tn)) { t = tn; break; }
+        const bool done = !fallback && fabs(tn - t) <= 1e-6 * fabs(tn);
         t = tn;
+        if (done) break;
     }
     return upper ? -t : t;
 }
 
-// b^ex for b >= 1 with ex = -m/2: exact-ish fast path used per quadrature node.
-// mode: m >= 0 -> half-integer fast path; m < 0 -> general exp(ex*log b).
+// 1/r for r > 0: hardware reciprocal + two Newton steps (~1 ulp; no IEEE div sequence).
+__device__ __forceinline__ double fast_rcp(double r) {
+    double y = __builtin_amdgcn_rcp(r);
+    y = fma(y, fma(-r, y, 1.0), y);
+    y = fma(y, fma(-r, y, 1.0), y);
+    return y;
+}
+
+// b^ex for b >= 1 with ex = -m/2 (m = node_m >= 0): squarings + one reciprocal;
+// m < 0 selects the general exp(ex * log b).  Used once per quadrature node.
 __device__ __forceinline__ double pow_node(double b, int m, double ex) {
     if (m >= 0) {
-        int k = m >> 1;
         double r = 1.0, s = b;
+        int k = m >> 1;
         while (k) { if (k & 1) r *= s; s *= s; k >>= 1; }
         if (m & 1) r *= sqrt(b);
-        return 1.0 / r;
+        if (!(r < 1.0e300)) return r == r ? 0.0 : r;     // overflow -> 0, NaN stays NaN
+        return fast_rcp(r);
     }
     return exp(ex * log(b));
 }
