@@ -10,6 +10,7 @@
 
 #include "cvq_common.h"
 #include "cvq_quad_kernels.h"
+#include "cvq_direct_kernels.h"
 
 namespace cvq {
 
@@ -170,8 +171,49 @@ void launch_slab_t(cvq_plan* p, const double* bounds, double* out) {
                        bounds, out);
 }
 
+// ---------------------------------------------------------------- DIRECT
+template <int COP, bool MSM, int QT>
+void launch_direct_q(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
+                     Header* hdr) {
+    const size_t lds = sizeof(double) * ((size_t)(5 + QT) * p->S.n + 4);
+    if (p->S.n <= 256)
+        hipLaunchKernelGGL((k_direct2<COP, MSM, QT, 1>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
+                           p->d_a, p->d_pi, mode, bounds, out, snaps, hdr);
+    else
+        hipLaunchKernelGGL((k_direct2<COP, MSM, QT, 2>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
+                           p->d_a, p->d_pi, mode, bounds, out, snaps, hdr);
+}
+
+template <int COP>
+void launch_direct_c(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
+                     Header* hdr) {
+    if (p->S.model != CVQ_MSM) { launch_direct_q<COP, false, 1>(p, P, mode, bounds, out, snaps, hdr); return; }
+    switch (p->S.q) {
+        case 1: launch_direct_q<COP, true, 1>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 2: launch_direct_q<COP, true, 2>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 3: launch_direct_q<COP, true, 3>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 4: launch_direct_q<COP, true, 4>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 5: launch_direct_q<COP, true, 5>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 6: launch_direct_q<COP, true, 6>(p, P, mode, bounds, out, snaps, hdr); break;
+        case 7: launch_direct_q<COP, true, 7>(p, P, mode, bounds, out, snaps, hdr); break;
+        default: launch_direct_q<COP, true, 8>(p, P, mode, bounds, out, snaps, hdr); break;
+    }
+}
+
+int launch_direct(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
+                  Header* hdr) {
+    switch (p->S.copula) {
+        case CVQ_GAUSSIAN: launch_direct_c<CVQ_GAUSSIAN>(p, P, mode, bounds, out, snaps, hdr); break;
+        case CVQ_STUDENT: launch_direct_c<CVQ_STUDENT>(p, P, mode, bounds, out, snaps, hdr); break;
+        default: launch_direct_c<CVQ_PLACKETT>(p, P, mode, bounds, out, snaps, hdr); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
+    if (p->strategy == CVQ_STRATEGY_DIRECT) return launch_direct(p, P, 0, nullptr, nullptr, snaps, hdr);
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
                 "prefix solve supports at most 4096 rows (3-D n <= 64)");
@@ -187,6 +229,10 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     TimedScope ts(p, TK_SLAB);
+    if (p->strategy == CVQ_STRATEGY_DIRECT) {
+        SolveConst P{};
+        return launch_direct(p, P, 1, bounds, out, nullptr, nullptr);
+    }
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
                 "prefix slab supports at most 4096 rows (3-D n <= 64)");
@@ -260,6 +306,7 @@ int dispatch_cop(cvq_plan* p, bool tables) {
 int ensure_mass(cvq_plan* p) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
+    if (p->strategy == CVQ_STRATEGY_DIRECT) return CVQ_OK;        // tables are built inside k_direct2
     if (!p->tables_valid) {
         TimedScope ts(p, TK_TABLES);
         int rc = dispatch_cop(p, true);
@@ -295,7 +342,7 @@ int check_args(const cvq_plan* p, const cvq_solve_args* a) {
     CVQ_REQUIRE(a != nullptr, CVQ_ERR_INVALID, "solve args is NULL");
     const double top = std::max({a->first_guess, a->second_guess_lo, a->second_guess_hi, a->max_var, a->min_var,
                                  a->lower});
-    CVQ_REQUIRE(!(top > p->v_cap), CVQ_ERR_RANGE,
+    CVQ_REQUIRE(p->strategy == CVQ_STRATEGY_DIRECT || !(top > p->v_cap), CVQ_ERR_RANGE,
                 "a VaR level in the solve arguments exceeds the plan's v_cap");
     CVQ_REQUIRE(a->tolerance > 0.0, CVQ_ERR_INVALID, "tolerance must be > 0");
     return CVQ_OK;
@@ -370,7 +417,10 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
                 CVQ_ERR_INVALID, "NULL static table");
     CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
     CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
-    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX, CVQ_ERR_UNSUPPORTED, "only the PREFIX strategy is built");
+    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX || s->strategy == CVQ_STRATEGY_DIRECT, CVQ_ERR_INVALID,
+                "unknown strategy");
+    CVQ_REQUIRE(!(s->strategy == CVQ_STRATEGY_DIRECT && s->dim != 2), CVQ_ERR_UNSUPPORTED,
+                "the DIRECT strategy is built for dim == 2");
     for (int l = 0; l < Q; ++l) {             // create_vol_combinations ij order (msm_estimation.py:384)
         int rem = l;
         for (int d = s->dim - 1; d >= 0; --d) {
@@ -562,9 +612,10 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
     const bool realloc = T > p->capT;
     if (realloc) {
         int rc;
-        if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi)) ||
-            (rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)) ||
-            (rc = dev_alloc(&p->d_C, (size_t)T * S.G)))
+        if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi))) return rc;
+        if (p->strategy == CVQ_STRATEGY_PREFIX &&
+            ((rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) ||
+             (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_C, (size_t)T * S.G))))
             return rc;
         p->capT = T;
     }
@@ -588,7 +639,7 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
 int32_t cvq_slab(cvq_plan* p, const double* bounds, double* out, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && bounds != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
-    if (mem != CVQ_MEM_DEVICE) {
+    if (mem != CVQ_MEM_DEVICE && p->strategy == CVQ_STRATEGY_PREFIX) {
         for (long long t = 0; t < 2 * p->T; ++t)
             CVQ_REQUIRE(!(bounds[t] > p->v_cap), CVQ_ERR_RANGE, "a bound exceeds the plan's v_cap");
     }

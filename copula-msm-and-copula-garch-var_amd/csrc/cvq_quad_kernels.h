@@ -47,31 +47,24 @@ __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __res
 //   B   = pdf / univariate-copula-margin-pdf      (MSM: pdf = 1; Plackett: B = pdf)
 // Layout [T][dim][n], coalesced along i.
 template <int COP, bool MSM>
-__global__ __launch_bounds__(256) void k_tables(StaticDev S, long long T, const double* __restrict__ a,
-                                                double* __restrict__ tA, double* __restrict__ tB) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long total = T * S.dim * S.n;
-    if (idx >= total) return;
-    const int i = (int)(idx % S.n);
-    const long long td = idx / S.n;
-    const int d = (int)(td % S.dim);
+__device__ __forceinline__ void table_entry(const StaticDev& S, const double* __restrict__ a, long long td, int d,
+                                            int i, double* A_out, double* B_out) {
     double u, pdf = 1.0;
     if (MSM) {
         const double* f = a + td * S.q;
         const double* ph = S.phi + (size_t)d * S.q * S.n + i;
         double acc = f[0] * ph[0];
         for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
-        u = acc;
+        u = acc;                                                 // msm_integration_function.py:34-36
     } else {
         const double sig = a[td];
         const double xs = S.x[i] / sig;                         // garch_integration_function.py:31
         u = 0.5 * (1.0 + erf(xs / kInvSqrt2));                   // :33
         pdf = (kInvSqrt2Pi * exp(-0.5 * (xs * xs))) / sig;       // :38
     }
-    double A, B;
     if (COP == CVQ_PLACKETT) {
-        A = u;
-        B = pdf;
+        *A_out = u;
+        *B_out = pdf;
     } else {
         double z, uni;
         if (COP == CVQ_STUDENT) {
@@ -81,9 +74,22 @@ __global__ __launch_bounds__(256) void k_tables(StaticDev S, long long T, const 
             z = ndtri(u);                                        // gaussian.py:44
             uni = kInvSqrt2Pi * exp(-0.5 * (z * z));             // gaussian.py:82
         }
-        A = z;
-        B = (1.0 / uni) * pdf;
+        *A_out = z;
+        *B_out = (1.0 / uni) * pdf;
     }
+}
+
+template <int COP, bool MSM>
+__global__ __launch_bounds__(256) void k_tables(StaticDev S, long long T, const double* __restrict__ a,
+                                                double* __restrict__ tA, double* __restrict__ tB) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = T * S.dim * S.n;
+    if (idx >= total) return;
+    const int i = (int)(idx % S.n);
+    const long long td = idx / S.n;
+    const int d = (int)(td % S.dim);
+    double A, B;
+    table_entry<COP, MSM>(S, a, td, d, i, &A, &B);
     tA[idx] = A;
     tB[idx] = B;
 }

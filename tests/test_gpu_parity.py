@@ -70,10 +70,20 @@ def test_special_functions_vs_scipy_and_mpmath():
     assert np.max(np.abs(got - k["erf"])) <= 2.3e-16
 
 
+STRATEGIES = ["prefix", "direct"]
+
+
+def _skip_unsupported(z, strategy):
+    if strategy == "direct" and int(z["dim"]) != 2:
+        pytest.skip("DIRECT strategy is built for dim == 2")
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES)
 @pytest.mark.parametrize("case", GOLDEN_CASES)
-def test_slab_integrals_match_reference(case):
+def test_slab_integrals_match_reference(case, strategy):
     z = load_golden(case)
-    p = _plan(z)
+    _skip_unsupported(z, strategy)
+    p = _plan(z, strategy=strategy)
     try:
         for i, (b, ref) in enumerate(golden_calls(z)):
             got = p.compute_integral(b)
@@ -82,10 +92,12 @@ def test_slab_integrals_match_reference(case):
         p.close()
 
 
+@pytest.mark.parametrize("strategy", STRATEGIES)
 @pytest.mark.parametrize("case", GOLDEN_CASES)
-def test_calc_var_matches_reference(case):
+def test_calc_var_matches_reference(case, strategy):
     z = load_golden(case)
-    p = _plan(z)
+    _skip_unsupported(z, strategy)
+    p = _plan(z, strategy=strategy)
     try:
         var, iters = p.calc_var(float(z["ptf_mean"]), **golden_kwargs(z))
     finally:
