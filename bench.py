@@ -10,13 +10,15 @@ after which every rank finalises the full VaR vector).
 
 One "step" = the calc_var-equivalent scope (utils/calc_var_class.py:95-177) over
 the batch, with the per-date forecast tables already resident in HBM:
-  set per-date inputs (device copy) -> marginal/special-function tables ->
-  joint-mass row prefixes -> per-date bisection solve -> [all-gather] -> finalise.
+  set per-date inputs (device copy) -> marginal/special-function tables (k_tables)
+  -> per-date slab-on-the-fly bisection solve (k_direct; DIRECT strategy, the
+  default) -> [all-gather] -> finalise (k_finalize).
+  (--strategy prefix: k_tables -> joint-mass row prefixes k_mass -> k_solve_prefix.)
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline     -- dominant kernel (joint-mass/prefix, k_mass), HIP-event timed
+  roofline     -- dominant kernel (k_direct, or k_mass for PREFIX), HIP-event timed
                   on the plan's stream; algorithmic bytes = 8 B x reachable nodes
-                  x dates per launch.
+                  x dates per launch, plus an FP64 sub-object.
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
 """
@@ -45,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
-    ap.add_argument("--strategy", default="prefix", choices=["prefix", "direct"])
+    ap.add_argument("--strategy", default="direct", choices=["prefix", "direct"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
     ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
@@ -189,7 +191,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_mass (joint-mass row prefix)" if dom == "mass"
-                                   else "k_direct2 (fused tables + per-date solve)",
+                                   else "k_direct (per-date slab-on-the-fly solve)",
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_us": dom_avg_s * 1e6,
                          "reach_nodes_per_date": plan.reach_nodes,
                          "fp64": {"achieved_tflops": fp64_tflops, "peak_tflops": FP64_PEAK_TFLOPS,

@@ -74,6 +74,7 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_plan_info": (i32, [v, C.POINTER(i64), _ip]),
         "cvq_plan_timing": (i32, [v, i32]),
         "cvq_plan_kernel_time": (i32, [v, i32, C.POINTER(d), _ip]),
+        "cvq_plan_debug_stamps": (i32, [v, v, i64]),
         "cvq_set_dates": (i32, [v, i64, v, v, i32]),
         "cvq_slab": (i32, [v, v, v, i32]),
         "cvq_solve": (i32, [v, C.POINTER(CvqSolveArgs), v, _ip, i32]),
@@ -89,6 +90,8 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_special": (i32, [i32, i32, d, v, i64, v, i32]),
     }
     for name, (res, args) in sig.items():
+        if name == "cvq_plan_debug_stamps" and not hasattr(lib, name):
+            continue                                   # diagnostic-only symbol (older builds)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -20,6 +20,7 @@ struct StaticDev {
     int node_m;                   // pow fast-path code for -(nu+dim)/2 (see pow_node)
     double node_ex;               // -(nu+dim)/2
     double uni_ex;                // -(nu+1)/2
+    int uni_m;                    // 2 * (nu+1)/2 when a half-integer <= 16, else -1
     double term1;                 // multivariate density constant (student.py:138 / gaussian.py:107)
     double g_uni;                 // univariate t constant (student.py:164)
     double inv_nu, nu, theta;

@@ -4,8 +4,8 @@
 // per date; each slab (a, b] is a set of contiguous inner-axis index ranges,
 // one per outer row (create_grids.py:102-108).  Here one 256-thread workgroup
 // per date
-//   1. evaluates the date's marginal / quantile tables straight into LDS
-//      (same code as k_tables),
+//   1. stages the date's inner-axis tables (k_tables output) into LDS and its
+//      outer-axis row constants into registers,
 //   2. walks calc_var's control flow (Q1-Q4) exactly as k_solve_prefix does,
 //      but sums each slab's nodes on the fly instead of reading prefix sums:
 //      thread = outer row, serial loop over that row's column range, node
@@ -17,58 +17,85 @@
 
 namespace cvq {
 
-__device__ __forceinline__ double pow_node_fast(double b, int m, double ex) {
-    // -(nu+d)/2 = -4 (nu=6, d=2) and -4.5 (nu=6, d=3) are the common cases
-    if (m == 8) { const double b2 = b * b; const double r = b2 * b2; return r < 1e300 ? fast_rcp(r) : 0.0; }
-    if (m == 9) { const double b2 = b * b; const double r = b2 * b2 * sqrt(b); return r < 1e300 ? fast_rcp(r) : 0.0; }
-    return pow_node(b, m, ex);
+// b^-(m/2) for b >= 1 with a compile-time m (PM > 0), branch-free; PM == 0: runtime.
+template <int PM>
+__device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
+    if constexpr (PM == 0) {
+        return pow_node(b, m, ex);
+    } else {
+        constexpr int k = PM >> 1;
+        double r = 1.0, s = b;
+#pragma unroll
+        for (int bit = 0; bit < 6; ++bit) {
+            if ((k >> bit) & 1) r *= s;
+            if ((k >> (bit + 1)) == 0) break;
+            s *= s;
+        }
+        if constexpr (PM & 1) r *= sqrt(b);
+        const double y = fast_rcp(r);
+        return (r < 1.0e300) ? y : 0.0;          // overflow -> 0; NaN propagates through r
+    }
 }
 
-template <int COP, bool MSM, int DIM>
+// Node value (node_value semantics) without data-dependent branches.
+template <int COP, bool MSM, int PM>
 __device__ __forceinline__ double node_value_d(const StaticDev& S, const RowCtx& r, double zc, double Bc, double W) {
-    if (COP != CVQ_STUDENT) return node_value<COP, MSM, DIM>(S, r, zc, Bc, W);
-    const double y0 = fma(zc, S.Ri[2], r.p0);
-    const double y1 = fma(zc, S.Ri[3], r.p1);
-    const double qf = fma(y1, zc, y0 * r.z0);
-    const bool fin = r.fin && isfinite(zc);
-    const double mv = fin ? S.term1 * pow_node_fast(fma(qf, S.inv_nu, 1.0), S.node_m, S.node_ex) : 0.0;
-    const double c = mv * (r.B * Bc);
-    if (MSM) return c * W;
-    return nan_to_num(c) * W;
+    if constexpr (COP != CVQ_STUDENT) {
+        return node_value<COP, MSM, 2>(S, r, zc, Bc, W);
+    } else {
+        const double y0 = fma(zc, S.Ri[2], r.p0);
+        const double y1 = fma(zc, S.Ri[3], r.p1);
+        const double qf = fma(y1, zc, y0 * r.z0);
+        const double pw = pow_node_t<PM>(fma(qf, S.inv_nu, 1.0), S.node_m, S.node_ex);
+        const bool fin = r.fin && isfinite(zc);
+        const double mv = fin ? S.term1 * pw : 0.0;   // student.py:133-141 (select, not branch)
+        const double c = mv * (r.B * Bc);
+        if (MSM) return c * W;
+        return nan_to_num(c) * W;
+    }
 }
 
-// mode 0: calc_var solve (snapshots + header);  mode 1: one slab per date (compute_integral)
-template <int COP, bool MSM, int QT, int RPT>
-__global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, const double* __restrict__ a,
-                                                 const double* __restrict__ pi, int mode,
-                                                 const double* __restrict__ bounds, double* __restrict__ out,
-                                                 double* __restrict__ snaps, Header* hdr) {
+// mode 0: calc_var solve (snapshots + header);  mode 1: one slab per date (compute_integral);
+// mode 2: table staging + row setup only (profiling ablation).
+//
+// Thread `slot` of the 256-thread block owns rows slot + 256 k (k < RPT) for the
+// whole solve.  Row constants (outer table values, row weights G) live in
+// registers; per node only the column operands come from LDS, and the lanes of
+// a wave (consecutive rows) read near-consecutive columns along the slab's
+// anti-diagonal edge, so the reads are conflict-free.  Two independent node
+// chains per iteration give the FP64 pipe instruction-level parallelism.
+template <int COP, bool MSM, int QT, int RPT, int PM>
+__global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, const double* __restrict__ tA,
+                                                        const double* __restrict__ tB, const double* __restrict__ pi,
+                                                        int mode, const double* __restrict__ bounds,
+                                                        double* __restrict__ out, double* __restrict__ snaps,
+                                                        Header* hdr) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int n = S.n, tid = threadIdx.x;
+    constexpr int NT = 256;
+    const int n = S.n, tid = threadIdx.x, slot = tid;
     const long long t = blockIdx.x;
     double* sx = lds;
     double* cA = sx + n;
     double* cB = cA + n;
     double* cF = cB + n;              // [QT][n] inner-axis Delta factors
-    double* rA = cF + QT * n;
-    double* rB = rA + n;
-    double* red = rB + n;             // [4]
+    double* red = cF + QT * n;        // [2][NT / 64]
+    int parity = 0;
 
-    // 1. this date's tables (axis 0 -> rows, axis 1 -> columns)
-    for (int e = tid; e < 2 * n; e += 256) {
-        const int d = e / n, i = e - d * n;
-        double A, B;
-        table_entry<COP, MSM>(S, a, t * S.dim + d, d, i, &A, &B);
-        if (d == 0) { rA[i] = A; rB[i] = B; } else { cA[i] = A; cB[i] = B; }
-    }
-    for (int i = tid; i < n; i += 256) {
+    unsigned long long* stamps = (mode == 0 && out) ? (unsigned long long*)out + t * 32 : nullptr;
+    auto stamp = [&](int idx) {                      // diagnostic only (never in a timed run)
+        if (stamps && tid == 0) stamps[idx] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
+    const double* At = tA + t * 2 * n;              // k_tables output [T][2][n]
+    const double* Bt = tB + t * 2 * n;
+    for (int i = tid; i < n; i += NT) {
         sx[i] = S.x[i];
+        cA[i] = At[n + i];
+        cB[i] = Bt[n + i];
 #pragma unroll
         for (int b = 0; b < QT; ++b) cF[b * n + i] = S.F[((size_t)QT + b) * n + i];
     }
-    __syncthreads();
-
-    // 2. row contexts (row = outer index i0 = tid + 256 k)
+    // this thread's rows: context + row weights G[b] = sum_a pi[a][b] F0[a][r]
     const double* pit = pi + t * S.Q;
     RowCtx ctx[RPT];
     double G[RPT][QT];
@@ -76,43 +103,59 @@ __global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, cons
     bool has[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-        const int r = tid + 256 * k;
+        const int r = slot + 256 * k;
         has[k] = r < n;
-        const int i0 = has[k] ? r : 0;
-        ctx[k] = make_row<COP, 2>(S, rA[i0], 0.0, rB[i0]);
+        const int rr = has[k] ? r : 0;
+        ctx[k] = make_row<COP, 2>(S, At[rr], 0.0, Bt[rr]);
+        lev[k] = S.x[rr] * S.w1;                      // integration_algo.py:20 (2-D)
 #pragma unroll
         for (int b = 0; b < QT; ++b) {
             double g = 0.0;
 #pragma unroll
-            for (int a2 = 0; a2 < QT; ++a2) g = fma(pit[a2 * QT + b], S.F[(size_t)a2 * n + i0], g);
+            for (int a2 = 0; a2 < QT; ++a2) g = fma(pit[a2 * QT + b], S.F[(size_t)a2 * n + rr], g);
             G[k][b] = g;
         }
-        lev[k] = sx[i0] * S.w1;                       // integration_algo.py:20 (2-D)
+    }
+    __syncthreads();
+    stamp(1);
+    if (mode == 2) {
+        if (tid == 0) snaps[t * P.stride] = ctx[0].z0 + G[0][0] + cA[n - 1];
+        return;
     }
     auto cnt = [&](int k, double v, int klo, int khi) {
         const double g = (v - lev[k]) / S.w0;         // var_function (Q10), exact FP64
         return count_le(sx, g, klo, khi);
     };
-    auto rowsum = [&](int k, int k0, int k1) {
-        double s = 0.0;
-        for (int j = k0 + 1; j <= k1; ++j) {
-            double W = 0.0;
+    auto node = [&](int k, int j) {
+        double W = 0.0;
 #pragma unroll
-            for (int b = 0; b < QT; ++b) W = fma(G[k][b], cF[b * n + j], W);
-            s += node_value_d<COP, MSM, 2>(S, ctx[k], cA[j], cB[j], W);
-        }
-        return s;
+        for (int b = 0; b < QT; ++b) W = fma(G[k][b], cF[b * n + j], W);
+        return node_value_d<COP, MSM, PM>(S, ctx[k], cA[j], cB[j], W);
     };
-    auto slab = [&](double lo_v, double hi_v) {
-        double part = 0.0;
+    auto range_sum = [&](const int (&ka)[RPT], const int (&kb)[RPT]) {
+        double p0 = 0.0, p1 = 0.0;
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
-            if (!has[k]) continue;
-            const int ka = cnt(k, lo_v, 0, n - 1);
-            const int kb = cnt(k, hi_v, ka, n - 1);
-            if (kb > ka) part += rowsum(k, ka, kb);
+            const int len = has[k] ? kb[k] - ka[k] : 0;
+            if (len <= 0) continue;
+            int j = ka[k] + 1;
+            const int j1 = j + len;
+            for (; j + 1 < j1; j += 2) {
+                p0 += node(k, j);
+                p1 += node(k, j + 1);
+            }
+            if (j < j1) p0 += node(k, j);
         }
-        return TeamReduce<256>::sum(part, red);
+        return TeamReduce<NT>::sum(p0 + p1, red, parity);
+    };
+    auto slab = [&](double lo_v, double hi_v) {
+        int ka[RPT], kb[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            ka[k] = has[k] ? cnt(k, lo_v, 0, n - 1) : 0;
+            kb[k] = has[k] ? cnt(k, hi_v, ka[k], n - 1) : 0;
+        }
+        return range_sum(ka, kb);
     };
 
     if (mode == 1) {
@@ -121,12 +164,15 @@ __global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, cons
         return;
     }
     // (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
+    stamp(2);
     const double r0 = slab(P.lower, P.fg);
+    stamp(3);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
     const double nr = slab(nl, nu);
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
+    stamp(4);
     double lo = __builtin_nan(""), hi = __builtin_nan("");
     if (F > P.obj) { lo = P.vmin; hi = P.sg0; }
     if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; }
@@ -139,6 +185,7 @@ __global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, cons
         kLo[k] = has[k] ? cnt(k, lo, 0, n - 1) : 0;
         kHi[k] = has[k] ? cnt(k, hi, kLo[k], n - 1) : 0;
     }
+    stamp(5);
     // (iv) bisection (:250-309), Q2 / Q4 resolved across dates by k_finalize
     double prev = F, prevU = prevU0;
     int nt = -1;
@@ -148,15 +195,14 @@ __global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, cons
         const double mid = (lo + hi) / 2;
         if (tid == 0) sn[it] = mid;
         if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-        int kM[RPT];
-        double part = 0.0;
+        int kM[RPT], ka[RPT], kb[RPT];
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             kM[k] = has[k] ? cnt(k, mid, kLo[k], kHi[k]) : 0;
-            if (ustack) { if (kM[k] > kLo[k]) part += rowsum(k, kLo[k], kM[k]); }   // (lo, mid]
-            else        { if (kHi[k] > kM[k]) part += rowsum(k, kM[k], kHi[k]); }   // (mid, hi]
+            ka[k] = ustack ? kLo[k] : kM[k];               // (lo, mid]  or  (mid, hi]
+            kb[k] = ustack ? kM[k] : kHi[k];
         }
-        const double val = TeamReduce<256>::sum(part, red);
+        const double val = range_sum(ka, kb);
         const double slab_lower = ustack ? lo : mid;
         const double Fn = (slab_lower == prevU) ? prev + val : prev - val;       // adjust_integral
         if (Fn != 0.0) mask |= (1ull << it);
@@ -168,6 +214,7 @@ __global__ __launch_bounds__(256) void k_direct2(StaticDev S, SolveConst P, cons
         }
         prev = Fn;
         prevU = mid;
+        if (it < 24) stamp(6 + it);
     }
     if (tid == 0) {
         sn[P.K] = (lo + hi) / 2;

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -25,6 +26,7 @@ int make_tconst(double nu, TConst* tk, double** d_cf) {
     tk->ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
     tk->ln_tail = tk->ln_k + (nu - 1) / 2 * tk->ln_nu - tk->ln_nu;
     tk->split = (tk->a + 1.0) / (tk->a + 2.5);
+    tk->ln_a = std::log(tk->a);
     std::vector<double> c(2 * kCfTerms);
     ibeta_cf_coeffs(tk->a, 0.5, c.data(), kCfTerms);
     ibeta_cf_coeffs(0.5, tk->a, c.data() + kCfTerms, kCfTerms);
@@ -70,6 +72,8 @@ struct cvq_plan {
     int* d_err = nullptr;
     long long capIO = 0;
     double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
+    unsigned long long* d_stamps = nullptr;   // diagnostic phase stamps (CVQ_STAMPS=1)
+    long long capStamps = 0;
     // optional per-kernel timing (HIP events on the plan's stream)
     bool timing = false;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> events;
@@ -172,16 +176,27 @@ void launch_slab_t(cvq_plan* p, const double* bounds, double* out) {
 }
 
 // ---------------------------------------------------------------- DIRECT
+template <int COP, bool MSM, int QT, int PM>
+void launch_direct_qp(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
+                      Header* hdr) {
+    const int rpt = p->S.n <= 256 ? 1 : 2;
+    const size_t lds = sizeof(double) * ((size_t)(3 + QT) * p->S.n + 8);
+    if (rpt == 1)
+        hipLaunchKernelGGL((k_direct<COP, MSM, QT, 1, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
+                           p->d_tA, p->d_tB, p->d_pi, mode, bounds, out, snaps, hdr);
+    else
+        hipLaunchKernelGGL((k_direct<COP, MSM, QT, 2, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
+                           p->d_tA, p->d_tB, p->d_pi, mode, bounds, out, snaps, hdr);
+}
+
 template <int COP, bool MSM, int QT>
 void launch_direct_q(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
                      Header* hdr) {
-    const size_t lds = sizeof(double) * ((size_t)(5 + QT) * p->S.n + 4);
-    if (p->S.n <= 256)
-        hipLaunchKernelGGL((k_direct2<COP, MSM, QT, 1>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_a, p->d_pi, mode, bounds, out, snaps, hdr);
-    else
-        hipLaunchKernelGGL((k_direct2<COP, MSM, QT, 2>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_a, p->d_pi, mode, bounds, out, snaps, hdr);
+    if constexpr (COP == CVQ_STUDENT) {
+        if (p->S.node_m == 8) { launch_direct_qp<COP, MSM, QT, 8>(p, P, mode, bounds, out, snaps, hdr); return; }
+        if (p->S.node_m == 9) { launch_direct_qp<COP, MSM, QT, 9>(p, P, mode, bounds, out, snaps, hdr); return; }
+    }
+    launch_direct_qp<COP, MSM, QT, 0>(p, P, mode, bounds, out, snaps, hdr);
 }
 
 template <int COP>
@@ -213,7 +228,21 @@ int launch_direct(cvq_plan* p, const SolveConst& P, int mode, const double* boun
 
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
-    if (p->strategy == CVQ_STRATEGY_DIRECT) return launch_direct(p, P, 0, nullptr, nullptr, snaps, hdr);
+    if (p->strategy == CVQ_STRATEGY_DIRECT) {
+        // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
+        static const int dbg_mode = getenv("CVQ_DIRECT_ABLATE") ? atoi(getenv("CVQ_DIRECT_ABLATE")) : 0;
+        static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
+        double* st = nullptr;
+        if (dbg_stamps) {
+            if (p->T > p->capStamps) {
+                if (p->d_stamps) (void)hipFree(p->d_stamps);
+                if (hipMalloc((void**)&p->d_stamps, (size_t)p->T * 32 * 8) != hipSuccess) p->d_stamps = nullptr;
+                p->capStamps = p->d_stamps ? p->T : 0;
+            }
+            st = (double*)p->d_stamps;
+        }
+        return launch_direct(p, P, dbg_mode == 2 ? 2 : 0, nullptr, st, snaps, hdr);
+    }
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
                 "prefix solve supports at most 4096 rows (3-D n <= 64)");
@@ -306,7 +335,6 @@ int dispatch_cop(cvq_plan* p, bool tables) {
 int ensure_mass(cvq_plan* p) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
-    if (p->strategy == CVQ_STRATEGY_DIRECT) return CVQ_OK;        // tables are built inside k_direct2
     if (!p->tables_valid) {
         TimedScope ts(p, TK_TABLES);
         int rc = dispatch_cop(p, true);
@@ -314,7 +342,7 @@ int ensure_mass(cvq_plan* p) {
         p->tables_valid = true;
         p->mass_valid = false;
     }
-    if (!p->mass_valid) {
+    if (!p->mass_valid && p->strategy == CVQ_STRATEGY_PREFIX) {
         TimedScope ts(p, TK_MASS);
         int rc = dispatch_cop(p, false);
         if (rc) return rc;
@@ -476,6 +504,8 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
             S.g_uni = std::tgamma((nu + 1) / 2) / (std::sqrt(nu * M_PI) * std::tgamma(nu / 2)); // :164
             S.node_ex = -(nu + d) / 2;
             S.uni_ex = -(nu + 1) / 2;
+            const double mu = nu + 1;
+            S.uni_m = (mu == std::floor(mu) && mu <= 16.0) ? (int)mu : -1;
             const double m2 = -2.0 * S.node_ex;
             S.node_m = (m2 == std::floor(m2) && m2 <= 128.0) ? (int)m2 : -1;
             if (int rc2 = make_tconst(nu, &S.tk, &p->d_cf)) { cvq_plan_destroy(p); return rc2; }
@@ -555,7 +585,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
-                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io})
+                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
@@ -601,6 +631,15 @@ int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_
     return CVQ_OK;
 }
 
+int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
+    CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(p->d_stamps != nullptr, CVQ_ERR_STATE, "no stamps recorded (set CVQ_STAMPS=1, DIRECT strategy)");
+    CVQ_REQUIRE(count <= p->capStamps * 32, CVQ_ERR_INVALID, "count exceeds the stamp buffer");
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    CVQ_HIP_CHECK(hipMemcpy(host, p->d_stamps, count * 8, hipMemcpyDeviceToHost));
+    return CVQ_OK;
+}
+
 int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && a != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(T > 0, CVQ_ERR_INVALID, "T must be > 0");
@@ -613,10 +652,9 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
     if (realloc) {
         int rc;
         if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi))) return rc;
-        if (p->strategy == CVQ_STRATEGY_PREFIX &&
-            ((rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) ||
-             (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_C, (size_t)T * S.G))))
+        if ((rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)))
             return rc;
+        if (p->strategy == CVQ_STRATEGY_PREFIX && (rc = dev_alloc(&p->d_C, (size_t)T * S.G))) return rc;
         p->capT = T;
     }
     p->T = T;

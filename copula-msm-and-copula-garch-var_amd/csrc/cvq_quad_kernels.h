@@ -22,10 +22,34 @@ constexpr double kInvSqrt2 = 1.4142135623730951;      // np.sqrt(2): divided by,
 constexpr double kInvSqrt2Pi = 0.3989422804014327;    // 1 / np.sqrt(2 * np.pi)
 
 // ------------------------------------------------------------------ wave helpers
+// DPP lane exchange of a double (two 32-bit halves); CTRL is a gfx9 dpp_ctrl code.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// Wave-wide sum, identical (bitwise) in every lane: symmetric DPP exchanges within
+// rows of 16 (xor 1, xor 2, half-mirror, mirror), then the four row sums combined
+// in a fixed order.  No LDS traffic.
 __device__ __forceinline__ double wave_sum(double v) {
+#ifdef CVQ_SHFL_REDUCE
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+#endif
+    v += dpp_f64<0xB1>(v);      // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);      // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);     // row_half_mirror
+    v += dpp_f64<0x140>(v);     // row_mirror
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 // -------------------------------------------------------- static Phi (MSM only)
@@ -69,7 +93,7 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
         double z, uni;
         if (COP == CVQ_STUDENT) {
             z = stdtrit(S.tk, u);                                // student.py:102
-            uni = isfinite(z) ? S.g_uni * pow(1.0 + (z * z) / S.nu, S.uni_ex) : 0.0;   // :164-172
+            uni = isfinite(z) ? S.g_uni * pow_half_neg(1.0 + (z * z) / S.nu, S.uni_m, S.uni_ex) : 0.0;   // :164-172
         } else {
             z = ndtri(u);                                        // gaussian.py:44
             uni = kInvSqrt2Pi * exp(-0.5 * (z * z));             // gaussian.py:82
@@ -272,16 +296,20 @@ __global__ __launch_bounds__(64) void k_mass(StaticDev S, const double* __restri
 // Team of TPD threads per date; thread owns rows r = tid + i*TPD (i < RPT).
 template <int TPD>
 struct TeamReduce {
-    __device__ static double sum(double v, double* red) {
+    // red: 2 * (TPD / 64) doubles; parity alternates the half used, so one
+    // barrier per reduction suffices (a half is rewritten only after every wave
+    // has passed the next reduction's barrier, i.e. finished reading it).
+    __device__ static double sum(double v, double* red, int& parity) {
         v = wave_sum(v);
         if (TPD == 64) return v;
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        double* r = red + parity * (TPD / 64);
+        parity ^= 1;
+        if (lane == 0) r[wave] = v;
         __syncthreads();
-        if (lane == 0) red[wave] = v;
-        __syncthreads();
-        double s = red[0];
+        double s = r[0];
 #pragma unroll
-        for (int w = 1; w < TPD / 64; ++w) s += red[w];
+        for (int w = 1; w < TPD / 64; ++w) s += r[w];
         return s;
     }
 };
@@ -310,6 +338,7 @@ struct SolveTeam {
     const double* sx;
     const double* Cd;      // this date's prefix block
     double* red;
+    int parity = 0;
     double s[RPT];
     int kmx[RPT];
     long long off[RPT];
@@ -346,7 +375,7 @@ struct SolveTeam {
             const int kb = count(i, b, 0, kmx[i]);
             if (kb > ka) part += pref(i, kb) - pref(i, ka);
         }
-        return TeamReduce<TPD>::sum(part, red);
+        return TeamReduce<TPD>::sum(part, red, parity);
     }
 };
 
@@ -357,7 +386,7 @@ template <int TPD, int RPT>
 __global__ __launch_bounds__(TPD) void k_solve_prefix(StaticDev S, SolveConst P, const double* __restrict__ C,
                                                       double* __restrict__ snaps, Header* hdr) {
     __shared__ double sx[512];
-    __shared__ double red[TPD / 64 > 0 ? TPD / 64 : 1];
+    __shared__ double red[2 * (TPD / 64 > 0 ? TPD / 64 : 1)];
     for (int j = threadIdx.x; j < S.n; j += TPD) sx[j] = S.x[j];
     __syncthreads();
     const long long t = blockIdx.x;
@@ -407,7 +436,7 @@ __global__ __launch_bounds__(TPD) void k_solve_prefix(StaticDev S, SolveConst P,
             if (ustack) { if (kM[i] > kLo[i]) part += cM[i] - cLo[i]; }   // slab (lo, mid]
             else        { if (kHi[i] > kM[i]) part += cHi[i] - cM[i]; }   // slab (mid, hi]
         }
-        const double val = TeamReduce<TPD>::sum(part, red);
+        const double val = TeamReduce<TPD>::sum(part, red, tm.parity);
         const double slab_lower = ustack ? lo : mid;
         const double Fn = (slab_lower == prevU) ? prev + val : prev - val;     // adjust_integral
         if (Fn != 0.0) mask |= (1ull << k);                                      // Q4
@@ -435,7 +464,7 @@ template <int TPD, int RPT>
 __global__ __launch_bounds__(TPD) void k_slab_prefix(StaticDev S, const double* __restrict__ C,
                                                      const double* __restrict__ bounds, double* __restrict__ out) {
     __shared__ double sx[512];
-    __shared__ double red[TPD / 64 > 0 ? TPD / 64 : 1];
+    __shared__ double red[2 * (TPD / 64 > 0 ? TPD / 64 : 1)];
     for (int j = threadIdx.x; j < S.n; j += TPD) sx[j] = S.x[j];
     __syncthreads();
     const long long t = blockIdx.x;

@@ -23,6 +23,7 @@ struct TConst {
     double ln_k;        // log of Gamma((nu+1)/2) / (sqrt(nu pi) Gamma(nu/2))
     double ln_tail;     // log(k_nu) + (nu-1)/2 log(nu) - log(nu): F(t) ~ exp(ln_tail) |t|^-nu
     double split;       // (a + 1) / (a + 1/2 + 2): continued-fraction branch point
+    double ln_a;        // log(a)
     const double* cf_dir;   // CF coefficients c_k of I_x(a, 1/2)   (d_k = c_k x), device
     const double* cf_cmp;   // CF coefficients c_k of I_y(1/2, a),  device
     int cf_terms;           // table length
@@ -82,7 +83,7 @@ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, doub
     if (x < k.split) {
         // F = 0.5 * I_x(a, 1/2) = 0.5 * x^a (1-x)^(1/2) / (a B) * cf
         const double ln1mx = ln_t2 - L;
-        *lnF = -0.69314718055994530942 + k.a * lnx + 0.5 * ln1mx - k.lbeta - log(k.a) +
+        *lnF = -0.69314718055994530942 + k.a * lnx + 0.5 * ln1mx - k.lbeta - k.ln_a +
                log(ibeta_cf(k.cf_dir, k.cf_terms, x));
     } else {
         // F = 0.5 * (1 - I_y(1/2, a)),  y = t^2 / (nu + t^2) small
@@ -93,6 +94,23 @@ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, doub
     }
 }
 
+// Acklam's rational approximation of the lower-half normal quantile (0 < pp <= 0.5),
+// relative error ~1e-9.
+__device__ __forceinline__ double ndtri_approx(double pp) {
+    if (pp < 0.02425) {
+        const double q = sqrt(-2.0 * log(pp));
+        return (((((-7.784894002430293e-03 * q - 3.223964580411365e-01) * q - 2.400758277161838e+00) * q -
+                  2.549732539343734e+00) * q + 4.374664141464968e+00) * q + 2.938163982698783e+00) /
+               ((((7.784695709041462e-03 * q + 3.224671290700398e-01) * q + 2.445134137142996e+00) * q +
+                 3.754408661907416e+00) * q + 1.0);
+    }
+    const double q = pp - 0.5, r = q * q;
+    return (((((-3.969683028665376e+01 * r + 2.209460984245205e+02) * r - 2.759285104469687e+02) * r +
+              1.383577518672690e+02) * r - 3.066479806614716e+01) * r + 2.506628277459239e+00) * q /
+           (((((-5.447609879822406e+01 * r + 1.615858368580409e+02) * r - 1.556989798598866e+02) * r +
+              6.680131188771972e+01) * r - 1.328068155288572e+01) * r + 1.0);
+}
+
 // Standard normal quantile (scipy.special.ndtri semantics at 0/1).
 __device__ inline double ndtri(double p) {
     if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
@@ -100,21 +118,7 @@ __device__ inline double ndtri(double p) {
     if (p == 1.0) return pos_inf();
     const bool upper = p > 0.5;
     const double pp = upper ? (1.0 - p) : p;   // exact for p >= 0.5
-    // Rational initial approximation (Acklam), relative error ~1e-9.
-    double x;
-    if (pp < 0.02425) {
-        const double q = sqrt(-2.0 * log(pp));
-        x = (((((-7.784894002430293e-03 * q - 3.223964580411365e-01) * q - 2.400758277161838e+00) * q -
-               2.549732539343734e+00) * q + 4.374664141464968e+00) * q + 2.938163982698783e+00) /
-            ((((7.784695709041462e-03 * q + 3.224671290700398e-01) * q + 2.445134137142996e+00) * q +
-              3.754408661907416e+00) * q + 1.0);
-    } else {
-        const double q = pp - 0.5, r = q * q;
-        x = (((((-3.969683028665376e+01 * r + 2.209460984245205e+02) * r - 2.759285104469687e+02) * r +
-               1.383577518672690e+02) * r - 3.066479806614716e+01) * r + 2.506628277459239e+00) * q /
-            (((((-5.447609879822406e+01 * r + 1.615858368580409e+02) * r - 1.556989798598866e+02) * r +
-               6.680131188771972e+01) * r - 1.328068155288572e+01) * r + 1.0);
-    }
+    double x = ndtri_approx(pp);                 // ~1e-9, refined below
     // Two Halley steps on Phi(x) = pp, Phi via erfc (relative accuracy in the tail).
     for (int it = 0; it < 2; ++it) {
         const double e = 0.5 * erfc(-x * 0.70710678118654752440) - pp;
@@ -135,7 +139,7 @@ __device__ inline double stdtrit(const TConst& k, double p) {
     const double nu = k.nu;
     double t;
     // Initial guess: Cornish-Fisher around the normal quantile, or the power tail.
-    const double z = ndtri(pp);
+    const double z = ndtri_approx(pp);           // only seeds the Cornish-Fisher guess
     const double z2 = z * z;
     double tcf = z + (z2 * z + z) / (4.0 * nu) +
                  (((5.0 * z2 + 16.0) * z2 + 3.0) * z) / (96.0 * nu * nu) +
@@ -195,6 +199,20 @@ __device__ __forceinline__ double pow_node(double b, int m, double ex) {
         return fast_rcp(r);
     }
     return exp(ex * log(b));
+}
+
+// b^(-m/2) for b >= 1, general m >= 0 (m < 0: exp(ex log b)); no loop for m <= 16.
+__device__ __forceinline__ double pow_half_neg(double b, int m, double ex) {
+    if (m < 0 || m > 16) return exp(ex * log(b));
+    const double b2 = b * b, b4 = b2 * b2, b8 = b4 * b4;
+    const int k = m >> 1;
+    double r = (k & 1) ? b : 1.0;
+    if (k & 2) r *= b2;
+    if (k & 4) r *= b4;
+    if (k & 8) r *= b8;
+    if (m & 1) r *= sqrt(b);
+    if (!(r < 1.0e300)) return r == r ? 0.0 : r;
+    return 1.0 / r;
 }
 
 __device__ __forceinline__ double nan_to_num(double v) {

@@ -106,6 +106,10 @@ int32_t cvq_plan_info(const cvq_plan* plan, int64_t* reach_nodes, int32_t* rows)
  * 4 slab.  cvq_plan_timing(enable) also clears previous records. */
 int32_t cvq_plan_timing(cvq_plan* plan, int32_t enable);
 int32_t cvq_plan_kernel_time(cvq_plan* plan, int32_t kind, double* total_ms, int32_t* launches);
+/* Diagnostic build aid: per-date phase timestamps (s_memtime) of the last DIRECT
+ * solve, recorded only when the process runs with CVQ_STAMPS=1 (never in a timed
+ * run).  host receives count uint64 values, 32 per date. */
+int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
 
 /* Per-date inputs = integrations_params_t (calc_integral.py:158):
  *   MSM:       a = forecasts_by_states [T][dim][q], b = forecasts [T][n_combos]
