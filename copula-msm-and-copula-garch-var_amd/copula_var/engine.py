@@ -34,7 +34,7 @@ class QuadraturePlan:
 
     def __init__(self, model: str, copula: str, dim: int, x_values, step, densities, combos, weights,
                  copula_params, vol_states=None, v_cap: float = 0.0, device: int = 0,
-                 strategy: str = "prefix"):
+                 strategy: str = "auto"):
         N.require_gpu()
         self.model, self.copula, self.dim = model, copula, int(dim)
         self.device = int(device)
@@ -60,7 +60,10 @@ class QuadraturePlan:
         st.vol_states = dp(self._vs) if self._vs is not None else None
         st.copula_params = dp(self._cp)
         st.n_copula_params = self._cp.size
+        if strategy == "auto":                          # DIRECT is built for 2 assets
+            strategy = "direct" if self.dim == 2 else "prefix"
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT}[strategy]
+        self.strategy = strategy
         st.v_cap = float(v_cap)
         self._static = st
         h = C.c_void_p()

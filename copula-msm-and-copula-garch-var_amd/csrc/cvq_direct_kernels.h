@@ -17,7 +17,10 @@
 
 namespace cvq {
 
-// b^-(m/2) for b >= 1 with a compile-time m (PM > 0), branch-free; PM == 0: runtime.
+// b^-(m/2) for b >= 1 with a compile-time m (PM > 0): squarings, hardware
+// reciprocal + one Newton step (v_rcp_f64 seeds >= 26 bits, so the step gives
+// ~1e-15 relative; the node tolerance is 1e-9); PM == 0: runtime m.
+// b = inf or NaN -> 0, exactly as pow_node's overflow rule.
 template <int PM>
 __device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
     if constexpr (PM == 0) {
@@ -32,26 +35,9 @@ __device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
             s *= s;
         }
         if constexpr (PM & 1) r *= sqrt(b);
-        const double y = fast_rcp(r);
-        return (r < 1.0e300) ? y : 0.0;          // overflow -> 0; NaN propagates through r
-    }
-}
-
-// Node value (node_value semantics) without data-dependent branches.
-template <int COP, bool MSM, int PM>
-__device__ __forceinline__ double node_value_d(const StaticDev& S, const RowCtx& r, double zc, double Bc, double W) {
-    if constexpr (COP != CVQ_STUDENT) {
-        return node_value<COP, MSM, 2>(S, r, zc, Bc, W);
-    } else {
-        const double y0 = fma(zc, S.Ri[2], r.p0);
-        const double y1 = fma(zc, S.Ri[3], r.p1);
-        const double qf = fma(y1, zc, y0 * r.z0);
-        const double pw = pow_node_t<PM>(fma(qf, S.inv_nu, 1.0), S.node_m, S.node_ex);
-        const bool fin = r.fin && isfinite(zc);
-        const double mv = fin ? S.term1 * pw : 0.0;   // student.py:133-141 (select, not branch)
-        const double c = mv * (r.B * Bc);
-        if (MSM) return c * W;
-        return nan_to_num(c) * W;
+        double y = __builtin_amdgcn_rcp(r);
+        y = fma(y, fma(-r, y, 1.0), y);
+        return (r < 1.0e300) ? y : 0.0;
     }
 }
 
@@ -88,19 +74,30 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     stamp(0);
     const double* At = tA + t * 2 * n;              // k_tables output [T][2][n]
     const double* Bt = tB + t * 2 * n;
+    // Student + MSM folds every per-node factor that is constant along a row or a
+    // column: node = b^-(nu+2)/2 * sum_b G'_b[r] F'_b[j] with F' = F * B_col and
+    // G' = G * term1 * B_row, and b = 1 + q/nu = R_r + z_j (P_r + C z_j).  A non-
+    // finite z makes b non-finite (pow -> 0) and its B infinite, so the node is
+    // 0 * inf = NaN exactly where student.py's 0/0 gives NaN (Q15, no guard on MSM).
+    constexpr bool FOLD = (COP == CVQ_STUDENT) && MSM;
     for (int i = tid; i < n; i += NT) {
         sx[i] = S.x[i];
         cA[i] = At[n + i];
-        cB[i] = Bt[n + i];
+        const double Bc = Bt[n + i];
+        cB[i] = Bc;
 #pragma unroll
-        for (int b = 0; b < QT; ++b) cF[b * n + i] = S.F[((size_t)QT + b) * n + i];
+        for (int b = 0; b < QT; ++b) {
+            const double f = S.F[((size_t)QT + b) * n + i];
+            cF[b * n + i] = FOLD ? f * Bc : f;
+        }
     }
     // this thread's rows: context + row weights G[b] = sum_a pi[a][b] F0[a][r]
     const double* pit = pi + t * S.Q;
     RowCtx ctx[RPT];
     double G[RPT][QT];
-    double lev[RPT];
+    double lev[RPT], Rr[RPT], Pr[RPT], Kr[RPT];
     bool has[RPT];
+    const double Cq = S.Ri[3] * S.inv_nu;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
         const int r = slot + 256 * k;
@@ -108,12 +105,16 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         const int rr = has[k] ? r : 0;
         ctx[k] = make_row<COP, 2>(S, At[rr], 0.0, Bt[rr]);
         lev[k] = S.x[rr] * S.w1;                      // integration_algo.py:20 (2-D)
+        const double z0 = ctx[k].z0;
+        Rr[k] = fma(S.Ri[0] * S.inv_nu, z0 * z0, 1.0);
+        Pr[k] = (S.Ri[1] + S.Ri[2]) * S.inv_nu * z0;
+        Kr[k] = S.term1 * ctx[k].B;
 #pragma unroll
         for (int b = 0; b < QT; ++b) {
             double g = 0.0;
 #pragma unroll
             for (int a2 = 0; a2 < QT; ++a2) g = fma(pit[a2 * QT + b], S.F[(size_t)a2 * n + rr], g);
-            G[k][b] = g;
+            G[k][b] = FOLD ? g * Kr[k] : g;
         }
     }
     __syncthreads();
@@ -130,7 +131,14 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         double W = 0.0;
 #pragma unroll
         for (int b = 0; b < QT; ++b) W = fma(G[k][b], cF[b * n + j], W);
-        return node_value_d<COP, MSM, PM>(S, ctx[k], cA[j], cB[j], W);
+        if constexpr (COP == CVQ_STUDENT) {
+            const double zc = cA[j];
+            const double pw = pow_node_t<PM>(fma(zc, fma(zc, Cq, Pr[k]), Rr[k]), S.node_m, S.node_ex);
+            if constexpr (MSM) return pw * W;                                 // msm_integration_function.py:45
+            return nan_to_num(pw * Kr[k] * cB[j]) * W;                        // garch_integration_function.py:45-50
+        } else {
+            return node_value<COP, MSM, 2>(S, ctx[k], cA[j], cB[j], W);
+        }
     };
     auto range_sum = [&](const int (&ka)[RPT], const int (&kb)[RPT]) {
         double p0 = 0.0, p1 = 0.0;

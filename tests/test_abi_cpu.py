@@ -1,0 +1,87 @@
+"""The C-ABI boundary without a GPU: libcvq.so loads, exports every function
+include/cvq.h declares, the ctypes mirrors match the header's structs, and
+argument validation that happens before any device work returns the
+documented status codes."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "cvq.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cvq_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_entry_points():
+    names = _declared()
+    for must in ("cvq_plan_create", "cvq_set_dates", "cvq_slab", "cvq_solve", "cvq_solve_local",
+                 "cvq_solve_finalize", "cvq_msm_filter", "cvq_garch_forecast", "cvq_ukf_forecast",
+                 "cvq_special", "cvq_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from copula_var import _native as N
+    lib = C.CDLL(N.LIB_PATH)
+    missing = [s for s in _declared() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_declares_every_symbol():
+    """_native._declare binds exactly the header's entry points."""
+    import inspect
+    from copula_var import _native as N
+    src = inspect.getsource(N._declare)
+    bound = set(re.findall(r'"(cvq_[a-z0-9_]+)"', src))
+    assert bound == set(_declared())
+
+
+def test_struct_layouts_match_header():
+    from copula_var import _native as N
+    # cvq_static: 6 int32, 7 pointers, int32 n_copula_params, int32 strategy, double v_cap
+    assert C.sizeof(N.CvqStatic) == 6 * 4 + 7 * 8 + 4 + 4 + 8
+    assert N.CvqStatic.v_cap.offset == 6 * 4 + 7 * 8 + 8
+    assert C.sizeof(N.CvqSolveArgs) == 9 * 8
+    hdr = open(HEADER).read()
+    for f, _ in N.CvqStatic._fields_:
+        assert re.search(rf"\b{f}\s*;", hdr), f
+    for f, _ in N.CvqSolveArgs._fields_:
+        assert re.search(rf"\b{f}\b", hdr), f
+
+
+def test_host_side_validation_without_gpu():
+    """Calls that fail argument checks before touching HIP return their status
+    codes and set cvq_last_error (no device needed)."""
+    from copula_var import _native as N
+    lib = N.lib()
+    assert lib.cvq_version() >= 1
+    # NULL static table -> invalid argument
+    h = C.c_void_p()
+    rc = lib.cvq_plan_create(None, 0, C.byref(h))
+    assert rc == N.CVQ_ERR_INVALID
+    assert lib.cvq_last_error()
+    # a solve budget beyond 62 bisection steps is rejected on the host
+    a = N.CvqSolveArgs(0.05, -3.0, -3.5, -2.0, -7.5, 0.0, -100.0, 1e-30, 0.0)
+    s = C.c_int32()
+    assert lib.cvq_snap_stride(C.byref(a), C.byref(s)) == N.CVQ_ERR_UNSUPPORTED
+    a.tolerance = 1e-6
+    assert lib.cvq_snap_stride(C.byref(a), C.byref(s)) == N.CVQ_OK
+    assert 20 <= s.value <= 30
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    """No CPU fallback: a missing libcvq.so raises instead of computing."""
+    import importlib
+    from copula_var import _native as N
+    monkeypatch.setattr(N, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(N, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        N.lib()

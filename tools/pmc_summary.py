@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes: per-kernel per-launch counter averages.
 
-Writes <outdir>/summary.json and, for the bench's dominant kernel (k_mass),
+Writes <outdir>/summary.json and, for the bench's dominant kernel (k_direct, or
+k_mass for --strategy prefix),
 profiles/pmc_traffic_cfg<N>.json with HBM bytes per launch, corrected as
 MI355X_MICROARCH.md §HBM says (FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE
 reads 1/2 of a wide streaming read on gfx950 -> doubled)."""
@@ -11,7 +12,7 @@ out = sys.argv[1]
 args = sys.argv[2:]
 cfg = 2
 dates = 1000
-strategy = "prefix"
+strategy = "direct"
 for i, a in enumerate(args):
     if a == "--config": cfg = int(args[i + 1])
     if a == "--dates-per-gpu": dates = int(args[i + 1])
@@ -32,7 +33,8 @@ for k, d in sorted(summ.items()):
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {v:16.1f}")
-mass = [k for k in summ if "k_mass" in k]
+dom = "k_mass" if strategy == "prefix" else "k_direct"
+mass = [k for k in summ if re.search(rf"\b{dom}\b", k)]
 if mass:
     d = summ[mass[0]]
     fetch = d.get("FETCH_SIZE", 0.0) * 1024 * 2
@@ -40,7 +42,8 @@ if mass:
     rec = {"kernel": mass[0], "config": cfg, "dates_per_launch": dates, "strategy": strategy,
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
-           "note": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide streaming reads); KiB -> bytes"}
+           "note": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide streaming reads); KiB -> bytes; "
+                   "the kernel's reads are 8-B/lane table loads, a width the guide leaves uncalibrated"}
     path = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", f"pmc_traffic_cfg{cfg}.json")
     json.dump(rec, open(path, "w"), indent=1)
     print(json.dumps(rec))
