@@ -104,24 +104,18 @@ def main():
         d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
         d_b, b_ptr = None, None
     args = engine.solve_args(ptf_mean)
-    stride = plan.snap_stride(args)
-    hdr = torch.zeros(2, dtype=torch.int64, device=dev)                  # 16-byte header
-    snaps = torch.full((per, stride), float("nan"), dtype=torch.float64, device=dev)
     var = torch.empty(T_total, dtype=torch.float64, device=dev)
     if world > 1:
-        hdr_all = torch.zeros(2 * world, dtype=torch.int64, device=dev)
-        snaps_all = torch.empty((T_total, stride), dtype=torch.float64, device=dev)
+        # rank-local solve -> one all-gather of headers + snapshots -> finalize (copula_var.distributed)
+        from copula_var.distributed import device_sharded_var
+        sharded = device_sharded_var(plan, args, T_total, dev)
 
     def step_fn():
-        plan.set_dates_device(per, d_a.data_ptr(), b_ptr)             # forces tables + mass recompute
+        plan.set_dates_device(per, d_a.data_ptr(), b_ptr)             # forces tables recompute
         if world == 1:
             plan.solve_device(args, var.data_ptr())
         else:
-            plan.solve_local(args, hdr.data_ptr(), snaps.data_ptr())
-            dist.all_gather_into_tensor(hdr_all, hdr)
-            dist.all_gather_into_tensor(snaps_all, snaps)
-            plan.solve_finalize(args, hdr_all.data_ptr(), world, snaps_all.data_ptr(), per, T_total,
-                                var.data_ptr())
+            sharded.solve()
 
     for _ in range(a.warmup):
         step_fn()
@@ -142,7 +136,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kt = {k: plan.kernel_time(k) for k in ("tables", "mass", "solve", "finalize")}
-    vals = var.cpu().numpy()
+    vals = (var if world == 1 else sharded.var).cpu().numpy()
     ms_step = elapsed / a.steps * 1e3
     value = T_total * a.steps / elapsed
 

@@ -87,6 +87,7 @@ class QuadraturePlan:
             pass
 
     def set_stream(self, stream_handle: Optional[int]) -> None:
+        """Launch on this HIP stream from now on (0 / None = the null stream, torch's default)."""
         N.check(N.lib().cvq_plan_set_stream(self._h, C.c_void_p(stream_handle or 0)), "cvq_plan_set_stream")
 
     KERNELS = {"tables": 0, "mass": 1, "solve": 2, "finalize": 3, "slab": 4}

@@ -12,6 +12,7 @@
 #include "cvq_common.h"
 #include "cvq_quad_kernels.h"
 #include "cvq_direct_kernels.h"
+#include "cvq_tppf_tables.h"
 
 namespace cvq {
 
@@ -24,17 +25,39 @@ int make_tconst(double nu, TConst* tk, double** d_cf) {
     tk->ln_nu = std::log(nu);
     tk->lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
     tk->ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
-    tk->ln_tail = tk->ln_k + (nu - 1) / 2 * tk->ln_nu - tk->ln_nu;
+    tk->ln_tail = tk->ln_k + (nu - 1) / 2 * tk->ln_nu;
     tk->split = (tk->a + 1.0) / (tk->a + 2.5);
     tk->ln_a = std::log(tk->a);
+    tk->inv_nu = 1.0 / nu;
+    tk->p_split = 0.05;
+    tk->tab_c = tk->tab_v = nullptr;
     std::vector<double> c(2 * kCfTerms);
     ibeta_cf_coeffs(tk->a, 0.5, c.data(), kCfTerms);
     ibeta_cf_coeffs(0.5, tk->a, c.data() + kCfTerms, kCfTerms);
-    CVQ_HIP_CHECK(hipMalloc((void**)d_cf, c.size() * sizeof(double)));
-    CVQ_HIP_CHECK(hipMemcpy(*d_cf, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    TConst hk = *tk;                                  // host copy for building the guess tables
+    hk.cf_dir = c.data();
+    hk.cf_cmp = c.data() + kCfTerms;
+    hk.cf_terms = kCfTerms;
+    std::vector<double> tab;
+    bool ok = false;
+    if (nu <= 1e5)
+        for (int nc = 256, nv = 64; nc <= 4096 && !ok; nc *= 2, nv *= 2) ok = build_tppf_tables(hk, nc, nv, tab);
+    if (!ok) tab.clear();
+    std::vector<double> all(c);
+    all.insert(all.end(), tab.begin(), tab.end());
+    CVQ_HIP_CHECK(hipMalloc((void**)d_cf, all.size() * sizeof(double)));
+    CVQ_HIP_CHECK(hipMemcpy(*d_cf, all.data(), all.size() * sizeof(double), hipMemcpyHostToDevice));
     tk->cf_dir = *d_cf;
     tk->cf_cmp = *d_cf + kCfTerms;
     tk->cf_terms = kCfTerms;
+    if (ok) {
+        tk->tab_c = *d_cf + 2 * kCfTerms;
+        tk->tab_v = tk->tab_c + 2 * (hk.n_c + 1);
+        tk->n_c = hk.n_c;
+        tk->n_v = hk.n_v;
+        tk->inv_hc = hk.inv_hc;
+        tk->inv_hv = hk.inv_hv;
+    }
     return CVQ_OK;
 }
 
@@ -582,6 +605,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     if (!p) return CVQ_OK;
     (void)hipSetDevice(p->device);
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
+    if (p->stream != p->own_stream) (void)hipStreamSynchronize(p->stream);   // work still using our buffers
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
@@ -594,7 +618,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
 
 int32_t cvq_plan_set_stream(cvq_plan* p, void* s) {
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
-    p->stream = s ? (hipStream_t)s : p->own_stream;
+    p->stream = (hipStream_t)s;                       // NULL = the HIP null stream
     return CVQ_OK;
 }
 

@@ -21,12 +21,21 @@ struct TConst {
     double ln_nu;       // log(nu)
     double lbeta;       // lgamma(nu/2) + lgamma(1/2) - lgamma(nu/2 + 1/2)
     double ln_k;        // log of Gamma((nu+1)/2) / (sqrt(nu pi) Gamma(nu/2))
-    double ln_tail;     // log(k_nu) + (nu-1)/2 log(nu) - log(nu): F(t) ~ exp(ln_tail) |t|^-nu
+    double ln_tail;     // log(k_nu) + (nu-1)/2 log(nu): F(t) ~ exp(ln_tail) |t|^-nu as t -> -inf
     double split;       // (a + 1) / (a + 1/2 + 2): continued-fraction branch point
     double ln_a;        // log(a)
     const double* cf_dir;   // CF coefficients c_k of I_x(a, 1/2)   (d_k = c_k x), device
     const double* cf_cmp;   // CF coefficients c_k of I_y(1/2, a),  device
     int cf_terms;           // table length
+    // Initial-guess tables for stdtrit (cubic Hermite, {value, derivative} pairs;
+    // nullptr = use the Cornish-Fisher / power-tail guess):
+    //   centre: t(p) on p in [p_split, 1/2], uniform in p;
+    //   tail:   g(v) = -1/t on v = p^(1/nu) in [0, p_split^(1/nu)], uniform in v
+    //           (1/|t| is analytic in v near 0: F ~ C |t|^-nu).
+    const double* tab_c;
+    const double* tab_v;
+    int n_c, n_v;           // intervals
+    double p_split, inv_hc, inv_hv, inv_nu;
 };
 
 // Host: continued-fraction coefficients of the regularised incomplete beta
@@ -40,12 +49,12 @@ inline void ibeta_cf_coeffs(double a, double b, double* c, int terms) {
     }
 }
 
-__device__ __forceinline__ double pos_inf() { return __builtin_huge_val(); }
+__host__ __device__ __forceinline__ double pos_inf() { return __builtin_huge_val(); }
 
 // 1/(1 + d1/(1 + d2/(1 + ...))), d_k = c[k-1] x, by the forward recurrence of
 // the convergents A_k / B_k (no division per term; the coefficient index is
 // wave-uniform, so c[] comes through the scalar cache).
-__device__ inline double ibeta_cf(const double* __restrict__ c, int terms, double x) {
+__host__ __device__ inline double ibeta_cf(const double* __restrict__ c, int terms, double x) {
     double Am = 1.0, Bm = 1.0;      // A_1, B_1
     double Ap = 0.0, Bp = 1.0;      // A_0, B_0
     for (int k = 1; k < terms; k += 2) {
@@ -64,7 +73,7 @@ __device__ inline double ibeta_cf(const double* __restrict__ c, int terms, doubl
 }
 
 // log F_nu(t) and log pdf_nu(t) for t <= 0.
-__device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, double* lpdf) {
+__host__ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, double* lpdf) {
     const double at = fabs(t);
     double L;                                   // log(nu + t^2)
     double ln_t2;                               // log(t^2)
@@ -96,7 +105,7 @@ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, doub
 
 // Acklam's rational approximation of the lower-half normal quantile (0 < pp <= 0.5),
 // relative error ~1e-9.
-__device__ __forceinline__ double ndtri_approx(double pp) {
+__host__ __device__ __forceinline__ double ndtri_approx(double pp) {
     if (pp < 0.02425) {
         const double q = sqrt(-2.0 * log(pp));
         return (((((-7.784894002430293e-03 * q - 3.223964580411365e-01) * q - 2.400758277161838e+00) * q -
@@ -128,32 +137,32 @@ __device__ inline double ndtri(double p) {
     return upper ? -x : x;
 }
 
-// Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
-__device__ inline double stdtrit(const TConst& k, double p) {
-    if (!(p >= 0.0 && p <= 1.0) || !(k.nu > 0.0)) return __builtin_nan("");
-    if (p == 0.0) return -pos_inf();
-    if (p == 1.0) return pos_inf();
-    if (p == 0.5) return 0.0;
-    const bool upper = p > 0.5;
-    const double pp = upper ? (1.0 - p) : p;   // exact
+// Cubic Hermite on uniform nodes: tab[2k] = y_k, tab[2k+1] = dy/dx_k, x in node units.
+__host__ __device__ __forceinline__ double hermite(const double* __restrict__ tab, int n, double x, double h) {
+    int k = (int)x;
+    k = k < 0 ? 0 : (k > n - 1 ? n - 1 : k);
+    const double s = x - k;
+    const double y0 = tab[2 * k], d0 = tab[2 * k + 1] * h, y1 = tab[2 * k + 2], d1 = tab[2 * k + 3] * h;
+    const double s2 = s * s, s3 = s2 * s;
+    return (2.0 * s3 - 3.0 * s2 + 1.0) * y0 + (s3 - 2.0 * s2 + s) * d0 + (3.0 * s2 - 2.0 * s3) * y1 + (s3 - s2) * d1;
+}
+
+// Initial guess for t.ppf at pp in (0, 1/2): the plan's Hermite tables (~1e-7
+// relative, so one Halley step of stdtrit lands at rounding level), else NaN.
+__host__ __device__ __forceinline__ double tppf_table_guess(const TConst& k, double pp) {
+    if (k.tab_c == nullptr) return __builtin_nan("");
+    if (pp >= k.p_split) return hermite(k.tab_c, k.n_c, (pp - k.p_split) * k.inv_hc, 1.0 / k.inv_hc);
+    const double v = exp(log(pp) * k.inv_nu);
+    const double g = hermite(k.tab_v, k.n_v, v * k.inv_hv, 1.0 / k.inv_hv);
+    return g > 0.0 ? -1.0 / g : __builtin_nan("");
+}
+
+// Halley on g(t) = log F(t) - lp for t < 0 (cubic convergence; stop once a step
+// is below 1e-6 relative: the next error is then ~1e-18).  Bisection fallback
+// whenever a step leaves the bracket F(lo) < p < F(hi).
+__host__ __device__ inline double tppf_refine(const TConst& k, double t, double lp) {
     const double nu = k.nu;
-    double t;
-    // Initial guess: Cornish-Fisher around the normal quantile, or the power tail.
-    const double z = ndtri_approx(pp);           // only seeds the Cornish-Fisher guess
-    const double z2 = z * z;
-    double tcf = z + (z2 * z + z) / (4.0 * nu) +
-                 (((5.0 * z2 + 16.0) * z2 + 3.0) * z) / (96.0 * nu * nu) +
-                 ((((3.0 * z2 + 19.0) * z2 + 17.0) * z2 - 15.0) * z) / (384.0 * nu * nu * nu);
-    // power tail F ~ exp(ln_tail)|t|^-nu (1 - nu^2 (nu+1) / (2 (nu+2) t^2)), two terms
-    double ttail = -exp((k.ln_tail - log(pp)) / nu);
-    ttail *= 1.0 - nu * (nu + 1.0) / (2.0 * (nu + 2.0) * ttail * ttail);
-    t = (ttail < tcf && z2 > nu) ? ttail : tcf;
-    if (nu > 1e5) return upper ? -tcf : tcf;
-    if (!(t < 0.0)) t = -1e-3;
-    const double lp = log(pp);
-    double lo = -pos_inf(), hi = 0.0;          // F(lo) < pp < F(hi)
-    // Halley on g(t) = log F(t) - log pp (cubic convergence; stop once a step is
-    // below 1e-6 relative: the next error is then ~1e-18).
+    double lo = -pos_inf(), hi = 0.0;
     for (int it = 0; it < 60; ++it) {
         double lnF, lpdf;
         t_lower_logs(k, t, &lnF, &lpdf);
@@ -176,6 +185,40 @@ __device__ inline double stdtrit(const TConst& k, double p) {
         t = tn;
         if (done) break;
     }
+    return t;
+}
+
+// Power-tail guess for log p = lp: F = exp(ln_tail)|t|^-nu (1 - A / t^2 + ...),
+// A = nu^2 (nu+1) / (2 (nu+2)), inverted to first order: t0 (1 - A / (nu t0^2)).
+__host__ __device__ __forceinline__ double tppf_tail_guess(const TConst& k, double lp) {
+    const double nu = k.nu;
+    double t = -exp((k.ln_tail - lp) / nu);
+    return t * (1.0 - nu * (nu + 1.0) / (2.0 * (nu + 2.0) * t * t));
+}
+
+// Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
+__host__ __device__ inline double stdtrit(const TConst& k, double p) {
+    if (!(p >= 0.0 && p <= 1.0) || !(k.nu > 0.0)) return __builtin_nan("");
+    if (p == 0.0) return -pos_inf();
+    if (p == 1.0) return pos_inf();
+    if (p == 0.5) return 0.0;
+    const bool upper = p > 0.5;
+    const double pp = upper ? (1.0 - p) : p;   // exact
+    const double nu = k.nu;
+    double t = tppf_table_guess(k, pp);        // the plan's tables: one Halley step
+    if (!(t < 0.0)) {
+        // Cornish-Fisher around the normal quantile, or the power tail.
+        const double z = ndtri_approx(pp);
+        const double z2 = z * z;
+        const double tcf = z + (z2 * z + z) / (4.0 * nu) +
+                           (((5.0 * z2 + 16.0) * z2 + 3.0) * z) / (96.0 * nu * nu) +
+                           ((((3.0 * z2 + 19.0) * z2 + 17.0) * z2 - 15.0) * z) / (384.0 * nu * nu * nu);
+        if (nu > 1e5) return upper ? -tcf : tcf;
+        const double ttail = tppf_tail_guess(k, log(pp));
+        t = (ttail < tcf && z2 > nu) ? ttail : tcf;
+        if (!(t < 0.0)) t = -1e-3;
+    }
+    t = tppf_refine(k, t, log(pp));
     return upper ? -t : t;
 }
 

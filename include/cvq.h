@@ -95,8 +95,10 @@ int32_t     cvq_device_count(int32_t* count);
 /* Plan = one device + one stream + device copies of the static tables. */
 int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out);
 int32_t cvq_plan_destroy(cvq_plan* plan);
-/* Run on an external stream (hipStream_t, e.g. torch.cuda.current_stream());
- * NULL restores the plan's own stream. */
+/* Run every later launch of the plan on hip_stream (a hipStream_t, e.g.
+ * torch.cuda.current_stream().cuda_stream).  NULL is the HIP null stream (torch's
+ * default stream), so the plan's work is ordered with the caller's; a new plan
+ * runs on a private non-blocking stream until this is called. */
 int32_t cvq_plan_set_stream(cvq_plan* plan, void* hip_stream);
 /* Reachable quadrature nodes per date (nodes with level <= v_cap in the box). */
 int32_t cvq_plan_info(const cvq_plan* plan, int64_t* reach_nodes, int32_t* rows);
