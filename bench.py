@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=0, help="also time the device forecast stage")
+    ap.add_argument("--time-all", type=int, default=0,
+                    help="HIP-event time every kernel kind (adds event records to the timed region)")
     return ap.parse_args()
 
 
@@ -120,7 +122,8 @@ def main():
     for _ in range(a.warmup):
         step_fn()
     torch.cuda.synchronize()
-    plan.enable_timing(True)
+    dom = "mass" if a.strategy == "prefix" else "solve"                       # dominant kernel
+    plan.enable_timing(True if a.time_all else (dom,))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -140,8 +143,7 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     value = T_total * a.steps / elapsed
 
-    # dominant kernel: k_mass (PREFIX) or the fused per-date solve k_direct2 (DIRECT)
-    dom = "mass" if a.strategy == "prefix" else "solve"
+    # dominant kernel: k_mass (PREFIX) or the per-date solve k_direct (DIRECT)
     dom_ms, dom_n = kt[dom]
     dom_avg_s = dom_ms / max(dom_n, 1) / 1e3
     alg_bytes = 8.0 * plan.reach_nodes * per          # one f64 joint-mass word per reachable node
@@ -158,7 +160,7 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items()}
+    kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items() if v[1]}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:

@@ -92,9 +92,16 @@ class QuadraturePlan:
 
     KERNELS = {"tables": 0, "mass": 1, "solve": 2, "finalize": 3, "slab": 4}
 
-    def enable_timing(self, on: bool = True) -> None:
-        """Record HIP events around every kernel launch on the plan's stream."""
-        N.check(N.lib().cvq_plan_timing(self._h, int(bool(on))), "cvq_plan_timing")
+    def enable_timing(self, on=True) -> None:
+        """Record HIP events around kernel launches on the plan's stream: True = every
+        kind, False = off, or an iterable of kind names (e.g. ("solve",))."""
+        if on is True or on is False:
+            mask = 0x1F if on else 0
+        else:
+            mask = 0
+            for k in on:
+                mask |= 1 << self.KERNELS[k]
+        N.check(N.lib().cvq_plan_timing(self._h, mask), "cvq_plan_timing")
 
     def kernel_time(self, kind: str) -> Tuple[float, int]:
         """(total milliseconds, launches) of one kernel kind since enable_timing()."""
@@ -120,7 +127,9 @@ class QuadraturePlan:
         self.T = int(T)
 
     def set_dates_device(self, T: int, a_ptr: int, b_ptr: Optional[int] = None) -> None:
-        """Per-date inputs already resident in device memory (e.g. torch tensors' data_ptr())."""
+        """Per-date inputs already resident in device memory (e.g. torch tensors' data_ptr()).
+        They are read in place by the following launches (no copy): keep them alive and
+        unchanged until the next set_dates."""
         N.check(N.lib().cvq_set_dates(self._h, int(T), C.c_void_p(a_ptr), C.c_void_p(b_ptr or 0), N.MEM_DEVICE),
                 "cvq_set_dates")
         self.T = int(T)

@@ -39,6 +39,11 @@ struct SolveConst {
     double obj, fg, sg0, sg1, vmin, vmax, lower, tol;
     int K;                        // bisection iterations executed (>= reference's count)
     int stride;                   // snapshot stride per date (K + 1)
+    // fused finalize (single-rank DIRECT solve): the last workgroup to finish
+    // resolves Q2/Q4 and writes fin_var[t] = snap[t][kstop] + ptf_mean.
+    double ptf_mean;
+    double* fin_var;              // nullptr: no fused finalize (sharded / PREFIX)
+    int* fin_err;                 // [4]: error, kstop, N, workgroup ticket (0 between launches)
 };
 
 struct alignas(16) Header {       // per-rank solve summary, all-gathered across ranks

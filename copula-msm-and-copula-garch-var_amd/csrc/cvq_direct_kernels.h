@@ -224,12 +224,37 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         prevU = mid;
         if (it < 24) stamp(6 + it);
     }
+    __shared__ int last;
     if (tid == 0) {
         sn[P.K] = (lo + hi) / 2;
         if (nt < 0 && !(hi - lo > P.tol)) nt = P.K;
         if (nt < 0) atomicOr(&hdr->error, 1);
         else atomicMax(&hdr->iters, nt);
         atomicOr((unsigned long long*)&hdr->nonzero, (unsigned long long)mask);
+        if (P.fin_var) {
+            __threadfence();                             // release: this date's snapshots + header bits
+            last = atomicAdd(&P.fin_err[3], 1) == (int)gridDim.x - 1;
+        }
+    }
+    if (!P.fin_var) return;
+    __syncthreads();
+    if (!last) return;
+    // k_finalize for a single rank, run by the last workgroup (calc_var_class.py:278, :293, :171)
+    __threadfence();                                     // acquire: every workgroup's stores
+    const int N = __hip_atomic_load(&hdr->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int e = __hip_atomic_load(&hdr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (N > P.K ? 2 : 0);
+    const unsigned long long nz = __hip_atomic_load((unsigned long long*)&hdr->nonzero, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    int kstop = min(N, P.K);
+    for (int k = 0; k < kstop; ++k)
+        if (!((nz >> k) & 1ull)) { kstop = k; break; }
+    for (long long d = tid; d < (long long)gridDim.x; d += NT)
+        P.fin_var[d] = snaps[d * P.stride + kstop] + P.ptf_mean;
+    if (tid == 0) {
+        P.fin_err[0] = e;
+        P.fin_err[1] = kstop;
+        P.fin_err[2] = N;
+        P.fin_err[3] = 0;                                // ticket reset for the next launch
     }
 }
 

@@ -84,6 +84,9 @@ struct cvq_plan {
     long long T = 0, capT = 0;
     double* d_a = nullptr;       // fbs [T][dim][q] or sigma [T][dim]
     double* d_pi = nullptr;      // [T][Q]  (GARCH/UKF: ones)
+    const double* in_a = nullptr;   // per-date inputs the kernels read: d_a / d_pi, or the
+    const double* in_pi = nullptr;  // caller's device buffers (cvq_set_dates with CVQ_MEM_DEVICE)
+    Header* zero_hdr = nullptr;     // header k_tables zeroes on its way (ensure_mass)
     double* d_tA = nullptr;      // [T][dim][n]
     double* d_tB = nullptr;
     double* d_C = nullptr;       // [T][G]
@@ -98,7 +101,7 @@ struct cvq_plan {
     unsigned long long* d_stamps = nullptr;   // diagnostic phase stamps (CVQ_STAMPS=1)
     long long capStamps = 0;
     // optional per-kernel timing (HIP events on the plan's stream)
-    bool timing = false;
+    int timing = 0;              // bitmask of kernel kinds timed with HIP events
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> events;
 };
 
@@ -110,7 +113,7 @@ struct TimedScope {
     int kind;
     hipEvent_t a = nullptr, b = nullptr;
     TimedScope(cvq_plan* p_, int kind_) : p(p_), kind(kind_) {
-        if (!p->timing) return;
+        if (!((p->timing >> kind) & 1)) return;
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
         (void)hipEventRecord(a, p->stream);
     }
@@ -206,10 +209,10 @@ void launch_direct_qp(cvq_plan* p, const SolveConst& P, int mode, const double* 
     const size_t lds = sizeof(double) * ((size_t)(3 + QT) * p->S.n + 8);
     if (rpt == 1)
         hipLaunchKernelGGL((k_direct<COP, MSM, QT, 1, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_tA, p->d_tB, p->d_pi, mode, bounds, out, snaps, hdr);
+                           p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr);
     else
         hipLaunchKernelGGL((k_direct<COP, MSM, QT, 2, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_tA, p->d_tB, p->d_pi, mode, bounds, out, snaps, hdr);
+                           p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr);
 }
 
 template <int COP, bool MSM, int QT>
@@ -302,14 +305,14 @@ template <int COP, bool MSM>
 void launch_tables_t(cvq_plan* p) {
     const long long total = p->T * p->S.dim * p->S.n;
     const unsigned blocks = (unsigned)((total + 255) / 256);
-    hipLaunchKernelGGL((k_tables<COP, MSM>), dim3(blocks), dim3(256), 0, p->stream, p->S, p->T, p->d_a, p->d_tA,
-                       p->d_tB);
+    hipLaunchKernelGGL((k_tables<COP, MSM>), dim3(blocks), dim3(256), 0, p->stream, p->S, p->T, p->in_a, p->d_tA,
+                       p->d_tB, p->zero_hdr);
 }
 
 template <int COP, bool MSM, int DIM, int QT>
 void launch_mass_q(cvq_plan* p) {
     const dim3 grid((unsigned)p->T, (unsigned)((p->S.nrows + 63) / 64));
-    hipLaunchKernelGGL((k_mass<COP, MSM, DIM, QT>), grid, dim3(64), 0, p->stream, p->S, p->d_tA, p->d_tB, p->d_pi,
+    hipLaunchKernelGGL((k_mass<COP, MSM, DIM, QT>), grid, dim3(64), 0, p->stream, p->S, p->d_tA, p->d_tB, p->in_pi,
                        p->d_C);
 }
 
@@ -355,15 +358,22 @@ int dispatch_cop(cvq_plan* p, bool tables) {
     return CVQ_OK;
 }
 
-int ensure_mass(cvq_plan* p) {
+// Brings tables (and PREFIX prefixes) up to date.  hdr, if given, is a solve
+// header to zero before the solve: folded into k_tables when that runs, else a
+// memset.
+int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
     if (!p->tables_valid) {
         TimedScope ts(p, TK_TABLES);
+        p->zero_hdr = hdr;
         int rc = dispatch_cop(p, true);
+        p->zero_hdr = nullptr;
         if (rc) return rc;
         p->tables_valid = true;
         p->mass_valid = false;
+    } else if (hdr) {
+        CVQ_HIP_CHECK(hipMemsetAsync(hdr, 0, sizeof(Header), p->stream));
     }
     if (!p->mass_valid && p->strategy == CVQ_STRATEGY_PREFIX) {
         TimedScope ts(p, TK_MASS);
@@ -386,6 +396,9 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.tol = a.tolerance;
     P.K = K;
     P.stride = K + 1;
+    P.ptf_mean = a.ptf_mean;
+    P.fin_var = nullptr;
+    P.fin_err = nullptr;
     return P;
 }
 
@@ -575,7 +588,8 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     p->stream = p->own_stream;
-    e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
+    e = hipMemset(p->d_err, 0, 4 * sizeof(int));         // error words + the fused-finalize ticket
+    if (e == hipSuccess) e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_kmax, kmax.data(), kmax.size() * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_off, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice);
@@ -633,7 +647,7 @@ int32_t cvq_plan_timing(cvq_plan* p, int32_t enable) {
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     p->events.clear();
-    p->timing = enable != 0;
+    p->timing = enable;
     return CVQ_OK;
 }
 
@@ -682,11 +696,19 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
         p->capT = T;
     }
     p->T = T;
-    const hipMemcpyKind kind = mem == CVQ_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_a, a, na * sizeof(double), kind, p->stream));
-    if (S.model == CVQ_MSM) {
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, b, npi * sizeof(double), kind, p->stream));
-    } else if (realloc) {                         // GARCH/UKF: pi_t = [1.0] (Q = 1), set once
+    if (mem == CVQ_MEM_DEVICE) {
+        // device-resident inputs are read in place by the next launches (no copy);
+        // the caller keeps them alive and unchanged until the next cvq_set_dates
+        p->in_a = a;
+        p->in_pi = S.model == CVQ_MSM ? b : p->d_pi;
+    } else {
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_a, a, na * sizeof(double), hipMemcpyHostToDevice, p->stream));
+        if (S.model == CVQ_MSM)
+            CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, b, npi * sizeof(double), hipMemcpyHostToDevice, p->stream));
+        p->in_a = p->d_a;
+        p->in_pi = p->d_pi;
+    }
+    if (S.model != CVQ_MSM && realloc) {          // GARCH/UKF: pi_t = [1.0] (Q = 1), set once
         std::vector<double> ones((size_t)p->capT * S.Q, 1.0);
         CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice,
                                      p->stream));
@@ -732,8 +754,7 @@ int32_t cvq_solve_local(cvq_plan* p, const cvq_solve_args* a, void* d_header, do
     if (rc) return rc;
     int32_t stride;
     if ((rc = cvq_snap_stride(a, &stride))) return rc;
-    if ((rc = ensure_mass(p))) return rc;
-    CVQ_HIP_CHECK(hipMemsetAsync(d_header, 0, sizeof(Header), p->stream));
+    if ((rc = ensure_mass(p, (Header*)d_header))) return rc;
     return launch_solve(p, solve_const(*a, stride - 1), d_snaps, (Header*)d_header);
 }
 
@@ -758,11 +779,11 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;
-    if ((rc = ensure_mass(p))) return rc;
+    if ((rc = ensure_mass(p, p->d_hdr))) return rc;
     bool exact;
     int K = bisect_budget(*a, &exact);
     if (!exact) K += 2;
-    for (;;) {
+    for (bool first = true;; first = false) {
         CVQ_REQUIRE(K <= kMaxIters, CVQ_ERR_NUMERIC, "bisection did not converge within 62 iterations");
         const int stride = K + 1;
         if ((rc = ensure_snap(p, p->T * stride))) return rc;
@@ -771,13 +792,20 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
             if ((rc = ensure_io(p, p->T))) return rc;
             d_var = p->d_io;
         }
-        CVQ_HIP_CHECK(hipMemsetAsync(p->d_hdr, 0, sizeof(Header), p->stream));
-        if ((rc = launch_solve(p, solve_const(*a, K), p->d_snap, p->d_hdr))) return rc;
-        const unsigned blocks = (unsigned)((p->T + 255) / 256);
-        TimedScope ts(p, TK_FINALIZE);
-        hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)p->d_hdr, 1,
-                           (const double*)p->d_snap, p->T, stride, K, a->ptf_mean, d_var, p->d_err);
-        CVQ_HIP_CHECK(hipGetLastError());
+        if (!first) CVQ_HIP_CHECK(hipMemsetAsync(p->d_hdr, 0, sizeof(Header), p->stream));
+        SolveConst P = solve_const(*a, K);
+        if (p->strategy == CVQ_STRATEGY_DIRECT) {       // finalize fused into the solve's last workgroup
+            P.fin_var = d_var;
+            P.fin_err = p->d_err;
+        }
+        if ((rc = launch_solve(p, P, p->d_snap, p->d_hdr))) return rc;
+        if (p->strategy != CVQ_STRATEGY_DIRECT) {
+            const unsigned blocks = (unsigned)((p->T + 255) / 256);
+            TimedScope ts(p, TK_FINALIZE);
+            hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)p->d_hdr, 1,
+                               (const double*)p->d_snap, p->T, stride, K, a->ptf_mean, d_var, p->d_err);
+            CVQ_HIP_CHECK(hipGetLastError());
+        }
         if (mem == CVQ_MEM_DEVICE && iters_out == nullptr) return CVQ_OK;
         int err[4] = {0, 0, 0, 0};
         CVQ_HIP_CHECK(hipMemcpyAsync(err, p->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, p->stream));

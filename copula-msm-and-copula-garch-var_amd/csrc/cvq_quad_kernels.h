@@ -105,8 +105,13 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
 
 template <int COP, bool MSM>
 __global__ __launch_bounds__(256) void k_tables(StaticDev S, long long T, const double* __restrict__ a,
-                                                double* __restrict__ tA, double* __restrict__ tB) {
+                                                double* __restrict__ tA, double* __restrict__ tB, Header* zero_hdr) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx == 0 && zero_hdr) {                     // the following solve's header (saves a memset launch)
+        zero_hdr->iters = 0;
+        zero_hdr->error = 0;
+        zero_hdr->nonzero = 0;
+    }
     const long long total = T * S.dim * S.n;
     if (idx >= total) return;
     const int i = (int)(idx % S.n);

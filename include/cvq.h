@@ -105,7 +105,8 @@ int32_t cvq_plan_info(const cvq_plan* plan, int64_t* reach_nodes, int32_t* rows)
 
 /* Per-kernel timing with HIP events recorded on the plan's stream (bench.py's
  * live roofline).  kind: 0 tables, 1 joint-mass/prefix, 2 solve, 3 finalize,
- * 4 slab.  cvq_plan_timing(enable) also clears previous records. */
+ * 4 slab.  cvq_plan_timing(mask) times the kinds whose bit (1 << kind) is set
+ * (0 = off, 0x1F = all) and clears previous records. */
 int32_t cvq_plan_timing(cvq_plan* plan, int32_t enable);
 int32_t cvq_plan_kernel_time(cvq_plan* plan, int32_t kind, double* total_ms, int32_t* launches);
 /* Diagnostic build aid: per-date phase timestamps (s_memtime) of the last DIRECT
@@ -115,7 +116,9 @@ int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
 
 /* Per-date inputs = integrations_params_t (calc_integral.py:158):
  *   MSM:       a = forecasts_by_states [T][dim][q], b = forecasts [T][n_combos]
- *   GARCH/UKF: a = sigma forecasts [T][dim],        b = NULL                 */
+ *   GARCH/UKF: a = sigma forecasts [T][dim],        b = NULL
+ * CVQ_MEM_HOST: copied.  CVQ_MEM_DEVICE: read in place by the following launches
+ * (no copy); the caller keeps a and b alive and unchanged until the next call. */
 int32_t cvq_set_dates(cvq_plan* plan, int64_t T, const double* a, const double* b, int32_t mem);
 
 /* Drop-in for ValueAtRiskCalcualtion.compute_integral (calc_var_class.py:179-212)
