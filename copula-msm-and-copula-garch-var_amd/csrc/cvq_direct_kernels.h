@@ -50,7 +50,10 @@ __device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
 // a wave (consecutive rows) read near-consecutive columns along the slab's
 // anti-diagonal edge, so the reads are conflict-free.  Two independent node
 // chains per iteration give the FP64 pipe instruction-level parallelism.
-template <int COP, bool MSM, int QT, int RPT, int PM>
+#ifndef CVQ_DIRECT_ILP
+#define CVQ_DIRECT_ILP 2
+#endif
+template <int COP, bool MSM, int QT, int RPT, int PM, int ILP = CVQ_DIRECT_ILP>
 __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, const double* __restrict__ tA,
                                                         const double* __restrict__ tB, const double* __restrict__ pi,
                                                         int mode, const double* __restrict__ bounds,
@@ -60,11 +63,15 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     constexpr int NT = 256;
     const int n = S.n, tid = threadIdx.x, slot = tid;
     const long long t = blockIdx.x;
-    double* sx = lds;
-    double* cA = sx + n;
-    double* cB = cA + n;
-    double* cF = cB + n;              // [QT][n] inner-axis Delta factors
-    double* red = cF + QT * n;        // [2][NT / 64]
+    // Column records, one per inner index j, CS doubles each (16-B aligned):
+    //   [0] z_j, [1..QT] F'_b[j], then B_j for the non-folded paths.
+    // A lane's operands for a node are CS contiguous doubles (ds_read_b128 x CS/2);
+    // lanes at consecutive j are CS*8 bytes apart, conflict-free for CS = 6.
+    constexpr bool FOLD = (COP == CVQ_STUDENT) && MSM;
+    constexpr int CS = ((1 + QT + (FOLD ? 0 : 1)) + 1) & ~1;
+    double* col = lds;                // [n][CS]
+    double* sx = col + CS * n;        // [n] grid
+    double* red = sx + n;             // [2][NT / 64]
     int parity = 0;
 
     unsigned long long* stamps = (mode == 0 && out) ? (unsigned long long*)out + t * 32 : nullptr;
@@ -79,17 +86,17 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     // G' = G * term1 * B_row, and b = 1 + q/nu = R_r + z_j (P_r + C z_j).  A non-
     // finite z makes b non-finite (pow -> 0) and its B infinite, so the node is
     // 0 * inf = NaN exactly where student.py's 0/0 gives NaN (Q15, no guard on MSM).
-    constexpr bool FOLD = (COP == CVQ_STUDENT) && MSM;
     for (int i = tid; i < n; i += NT) {
         sx[i] = S.x[i];
-        cA[i] = At[n + i];
+        double* c = col + i * CS;
+        c[0] = At[n + i];
         const double Bc = Bt[n + i];
-        cB[i] = Bc;
 #pragma unroll
         for (int b = 0; b < QT; ++b) {
             const double f = S.F[((size_t)QT + b) * n + i];
-            cF[b * n + i] = FOLD ? f * Bc : f;
+            c[1 + b] = FOLD ? f * Bc : f;
         }
+        if constexpr (!FOLD) c[1 + QT] = Bc;
     }
     // this thread's rows: context + row weights G[b] = sum_a pi[a][b] F0[a][r]
     const double* pit = pi + t * S.Q;
@@ -120,7 +127,7 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     __syncthreads();
     stamp(1);
     if (mode == 2) {
-        if (tid == 0) snaps[t * P.stride] = ctx[0].z0 + G[0][0] + cA[n - 1];
+        if (tid == 0) snaps[t * P.stride] = ctx[0].z0 + G[0][0] + col[(n - 1) * CS];
         return;
     }
     auto cnt = [&](int k, double v, int klo, int khi) {
@@ -128,33 +135,42 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         return count_le(sx, g, klo, khi);
     };
     auto node = [&](int k, int j) {
+        const double* c = col + j * CS;
         double W = 0.0;
 #pragma unroll
-        for (int b = 0; b < QT; ++b) W = fma(G[k][b], cF[b * n + j], W);
+        for (int b = 0; b < QT; ++b) W = fma(G[k][b], c[1 + b], W);
+        const double zc = c[0];
         if constexpr (COP == CVQ_STUDENT) {
-            const double zc = cA[j];
             const double pw = pow_node_t<PM>(fma(zc, fma(zc, Cq, Pr[k]), Rr[k]), S.node_m, S.node_ex);
             if constexpr (MSM) return pw * W;                                 // msm_integration_function.py:45
-            return nan_to_num(pw * Kr[k] * cB[j]) * W;                        // garch_integration_function.py:45-50
+            return nan_to_num(pw * Kr[k] * c[1 + QT]) * W;                    // garch_integration_function.py:45-50
         } else {
-            return node_value<COP, MSM, 2>(S, ctx[k], cA[j], cB[j], W);
+            return node_value<COP, MSM, 2>(S, ctx[k], zc, c[1 + QT], W);
         }
     };
     auto range_sum = [&](const int (&ka)[RPT], const int (&kb)[RPT]) {
-        double p0 = 0.0, p1 = 0.0;
+        // ILP independent node chains per thread (the slab's longest row is the
+        // workgroup's critical path, so per-row latency matters more than issue)
+        double p[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) p[u] = 0.0;
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int len = has[k] ? kb[k] - ka[k] : 0;
             if (len <= 0) continue;
             int j = ka[k] + 1;
             const int j1 = j + len;
-            for (; j + 1 < j1; j += 2) {
-                p0 += node(k, j);
-                p1 += node(k, j + 1);
+            for (; j + ILP - 1 < j1; j += ILP) {
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) p[u] += node(k, j + u);
             }
-            if (j < j1) p0 += node(k, j);
+            for (; j < j1; ++j) p[ILP - 1] += node(k, j);
         }
-        return TeamReduce<NT>::sum(p0 + p1, red, parity);
+#pragma unroll
+        for (int h = 1; h < ILP; h <<= 1)
+#pragma unroll
+            for (int u = 0; u + h < ILP; u += 2 * h) p[u] += p[u + h];
+        return TeamReduce<NT>::sum(p[0], red, parity);
     };
     auto slab = [&](double lo_v, double hi_v) {
         int ka[RPT], kb[RPT];

@@ -206,7 +206,9 @@ template <int COP, bool MSM, int QT, int PM>
 void launch_direct_qp(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
                       Header* hdr) {
     const int rpt = p->S.n <= 256 ? 1 : 2;
-    const size_t lds = sizeof(double) * ((size_t)(3 + QT) * p->S.n + 8);
+    constexpr bool fold = (COP == CVQ_STUDENT) && MSM;
+    constexpr int cs = ((1 + QT + (fold ? 0 : 1)) + 1) & ~1;      // k_direct's column record
+    const size_t lds = sizeof(double) * ((size_t)(cs + 1) * p->S.n + 8);
     if (rpt == 1)
         hipLaunchKernelGGL((k_direct<COP, MSM, QT, 1, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
                            p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr);
