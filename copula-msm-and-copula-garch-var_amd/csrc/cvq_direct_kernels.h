@@ -148,7 +148,61 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
             return node_value<COP, MSM, 2>(S, ctx[k], zc, c[1 + QT], W);
         }
     };
+    // Folded Student/MSM path: per row, acc_b = sum_j pw_j F'_b[j] and the row's
+    // sum is sum_b G'_b acc_b -- 12 FP64 ops per node (2 FMA quadratic form,
+    // RCP + 2 FMA Newton + 2 MUL for b^-4, QT FMA), no select: 1/b of an infinite
+    // or NaN b is NaN, which is what the node must be there (see above).
+    auto pw_fold = [&](int k, double zc) {
+        const double b = fma(zc, fma(zc, Cq, Pr[k]), Rr[k]);
+        if constexpr (PM == 8) {
+            double y = __builtin_amdgcn_rcp(b);
+            y = fma(y, fma(-b, y, 1.0), y);
+            const double y2 = y * y;
+            return y2 * y2;
+        } else {
+            return pow_node_t<PM>(b, S.node_m, S.node_ex);
+        }
+    };
+    auto range_sum_fold = [&](const int (&ka)[RPT], const int (&kb)[RPT]) {
+        double part = 0.0;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int len = has[k] ? kb[k] - ka[k] : 0;
+            if (len <= 0) continue;
+            double acc[ILP][QT];
+#pragma unroll
+            for (int u = 0; u < ILP; ++u)
+#pragma unroll
+                for (int b = 0; b < QT; ++b) acc[u][b] = 0.0;
+            int j = ka[k] + 1;
+            const int j1 = j + len;
+            for (; j + ILP - 1 < j1; j += ILP) {
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) {
+                    const double* c = col + (j + u) * CS;
+                    const double pw = pw_fold(k, c[0]);
+#pragma unroll
+                    for (int b = 0; b < QT; ++b) acc[u][b] = fma(pw, c[1 + b], acc[u][b]);
+                }
+            }
+            for (; j < j1; ++j) {
+                const double* c = col + j * CS;
+                const double pw = pw_fold(k, c[0]);
+#pragma unroll
+                for (int b = 0; b < QT; ++b) acc[0][b] = fma(pw, c[1 + b], acc[0][b]);
+            }
+#pragma unroll
+            for (int b = 0; b < QT; ++b) {
+                double a = acc[0][b];
+#pragma unroll
+                for (int u = 1; u < ILP; ++u) a += acc[u][b];
+                part = fma(G[k][b], a, part);
+            }
+        }
+        return TeamReduce<NT>::sum(part, red, parity);
+    };
     auto range_sum = [&](const int (&ka)[RPT], const int (&kb)[RPT]) {
+        if constexpr (FOLD) return range_sum_fold(ka, kb);
         // ILP independent node chains per thread (the slab's longest row is the
         // workgroup's critical path, so per-row latency matters more than issue)
         double p[ILP];
