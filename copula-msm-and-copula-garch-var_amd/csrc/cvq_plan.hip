@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -19,44 +21,86 @@ namespace cvq {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
-int make_tconst(double nu, TConst* tk, double** d_cf) {
-    tk->nu = nu;
-    tk->a = nu / 2;
-    tk->ln_nu = std::log(nu);
-    tk->lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
-    tk->ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
-    tk->ln_tail = tk->ln_k + (nu - 1) / 2 * tk->ln_nu;
-    tk->split = (tk->a + 1.0) / (tk->a + 2.5);
-    tk->ln_a = std::log(tk->a);
-    tk->inv_nu = 1.0 / nu;
-    tk->p_split = 0.05;
-    tk->tab_c = tk->tab_v = nullptr;
+// Host image of one nu's Student-t data: CF coefficients, cubic guess tables and
+// the direct (degree-5) tables, laid out as they are copied to the device.
+struct TImage {
+    TConst k{};                       // table pointers are offsets into `data` (as doubles)
+    std::vector<double> data;
+    long long off_tab = -1, off_q = -1;
+};
+
+static TImage build_timage(double nu) {
+    TImage im;
+    TConst& k = im.k;
+    k.nu = nu;
+    k.a = nu / 2;
+    k.ln_nu = std::log(nu);
+    k.lbeta = std::lgamma(nu / 2) + std::lgamma(0.5) - std::lgamma(nu / 2 + 0.5);
+    k.ln_k = std::lgamma((nu + 1) / 2) - std::lgamma(nu / 2) - 0.5 * std::log(nu * M_PI);
+    k.ln_tail = k.ln_k + (nu - 1) / 2 * k.ln_nu;
+    k.split = (k.a + 1.0) / (k.a + 2.5);
+    k.ln_a = std::log(k.a);
+    k.inv_nu = 1.0 / nu;
+    k.p_split = 0.05;
+    k.cf_terms = kCfTerms;
     std::vector<double> c(2 * kCfTerms);
-    ibeta_cf_coeffs(tk->a, 0.5, c.data(), kCfTerms);
-    ibeta_cf_coeffs(0.5, tk->a, c.data() + kCfTerms, kCfTerms);
-    TConst hk = *tk;                                  // host copy for building the guess tables
+    ibeta_cf_coeffs(k.a, 0.5, c.data(), kCfTerms);
+    ibeta_cf_coeffs(0.5, k.a, c.data() + kCfTerms, kCfTerms);
+    TConst hk = k;                                    // host evaluation copy
     hk.cf_dir = c.data();
     hk.cf_cmp = c.data() + kCfTerms;
-    hk.cf_terms = kCfTerms;
-    std::vector<double> tab;
-    bool ok = false;
+    std::vector<double> tab, quint;
+    bool ok = false, qok = false;
     if (nu <= 1e5)
         for (int nc = 256, nv = 64; nc <= 4096 && !ok; nc *= 2, nv *= 2) ok = build_tppf_tables(hk, nc, nv, tab);
-    if (!ok) tab.clear();
-    std::vector<double> all(c);
-    all.insert(all.end(), tab.begin(), tab.end());
-    CVQ_HIP_CHECK(hipMalloc((void**)d_cf, all.size() * sizeof(double)));
-    CVQ_HIP_CHECK(hipMemcpy(*d_cf, all.data(), all.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (ok)
+        for (int nc = 256; nc <= 4096 && !qok; nc *= 2) qok = build_tppf_quintic(hk, nc, nc < 1024 ? 128 : nc / 4, quint);
+    im.data = c;
+    if (ok) {
+        im.off_tab = (long long)im.data.size();
+        im.data.insert(im.data.end(), tab.begin(), tab.end());
+        k.n_c = hk.n_c;
+        k.n_v = hk.n_v;
+        k.inv_hc = hk.inv_hc;
+        k.inv_hv = hk.inv_hv;
+    }
+    if (qok) {
+        im.off_q = (long long)im.data.size();
+        im.data.insert(im.data.end(), quint.begin(), quint.end());
+        k.n_qc = hk.n_qc;
+        k.n_qv = hk.n_qv;
+        k.inv_qc = hk.inv_qc;
+        k.inv_qv = hk.inv_qv;
+    }
+    return im;
+}
+
+// Student-t constants for nu with device copies of its tables in *d_cf (owned by
+// the caller).  Table construction (~0.1 s for nu = 6) is cached per nu.
+int make_tconst(double nu, TConst* tk, double** d_cf) {
+    static std::mutex mu;
+    static std::map<double, TImage> cache;
+    const TImage* im;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(nu);
+        if (it == cache.end()) it = cache.emplace(nu, build_timage(nu)).first;
+        im = &it->second;
+    }
+    CVQ_HIP_CHECK(hipMalloc((void**)d_cf, im->data.size() * sizeof(double)));
+    CVQ_HIP_CHECK(hipMemcpy(*d_cf, im->data.data(), im->data.size() * sizeof(double), hipMemcpyHostToDevice));
+    *tk = im->k;
     tk->cf_dir = *d_cf;
     tk->cf_cmp = *d_cf + kCfTerms;
-    tk->cf_terms = kCfTerms;
-    if (ok) {
-        tk->tab_c = *d_cf + 2 * kCfTerms;
-        tk->tab_v = tk->tab_c + 2 * (hk.n_c + 1);
-        tk->n_c = hk.n_c;
-        tk->n_v = hk.n_v;
-        tk->inv_hc = hk.inv_hc;
-        tk->inv_hv = hk.inv_hv;
+    tk->tab_c = tk->tab_v = nullptr;
+    tk->q_c = tk->q_v = nullptr;
+    if (im->off_tab >= 0) {
+        tk->tab_c = *d_cf + im->off_tab;
+        tk->tab_v = tk->tab_c + 2 * (tk->n_c + 1);
+    }
+    if (im->off_q >= 0) {
+        tk->q_c = *d_cf + im->off_q;
+        tk->q_v = tk->q_c + 6 * tk->n_qc;
     }
     return CVQ_OK;
 }

@@ -36,6 +36,14 @@ struct TConst {
     const double* tab_v;
     int n_c, n_v;           // intervals
     double p_split, inv_hc, inv_hv, inv_nu;
+    // Direct evaluation tables (quintic Hermite in power form, 6 coefficients per
+    // interval in the local coordinate s in [0,1)), same variables as above;
+    // host-verified to 4e-14 relative, so stdtrit needs no refinement.  nullptr:
+    // not built (then the cubic guess + one Halley step is used).
+    const double* q_c;
+    const double* q_v;
+    int n_qc, n_qv;
+    double inv_qc, inv_qv;
 };
 
 // Host: continued-fraction coefficients of the regularised incomplete beta
@@ -53,53 +61,57 @@ __host__ __device__ __forceinline__ double pos_inf() { return __builtin_huge_val
 
 // 1/(1 + d1/(1 + d2/(1 + ...))), d_k = c[k-1] x, by the forward recurrence of
 // the convergents A_k / B_k (no division per term; the coefficient index is
-// wave-uniform, so c[] comes through the scalar cache).
-__host__ __device__ inline double ibeta_cf(const double* __restrict__ c, int terms, double x) {
-    double Am = 1.0, Bm = 1.0;      // A_1, B_1
-    double Ap = 0.0, Bp = 1.0;      // A_0, B_0
+// wave-uniform, so c[] comes through the scalar cache).  R = double on the
+// device; the host also runs it in long double to build the quantile tables.
+template <class R = double>
+__host__ __device__ inline R ibeta_cf(const double* __restrict__ c, int terms, R x) {
+    constexpr R tol = sizeof(R) > 8 ? (R)1e-19L : (R)1e-16;
+    R Am = 1, Bm = 1;               // A_1, B_1
+    R Ap = 0, Bp = 1;               // A_0, B_0
     for (int k = 1; k < terms; k += 2) {
-        double An = fma(c[k - 1] * x, Ap, Am), Bn = fma(c[k - 1] * x, Bp, Bm);
+        R An = fma((R)c[k - 1] * x, Ap, Am), Bn = fma((R)c[k - 1] * x, Bp, Bm);
         Ap = Am; Bp = Bm; Am = An; Bm = Bn;
-        An = fma(c[k] * x, Ap, Am); Bn = fma(c[k] * x, Bp, Bm);
+        An = fma((R)c[k] * x, Ap, Am); Bn = fma((R)c[k] * x, Bp, Bm);
         Ap = Am; Bp = Bm; Am = An; Bm = Bn;
-        // |A_k/B_k - A_{k-1}/B_{k-1}| <= 1e-16 |A_k/B_k|
-        if (fabs(fma(Am, Bp, -Ap * Bm)) <= 1e-16 * fabs(Am * Bp)) break;
-        if (fabs(Bm) > 1e150) {
-            const double s = 1.0 / Bm;
-            Am *= s; Ap *= s; Bp *= s; Bm = 1.0;
+        // |A_k/B_k - A_{k-1}/B_{k-1}| <= tol |A_k/B_k|
+        if (fabs(fma(Am, Bp, -Ap * Bm)) <= tol * fabs(Am * Bp)) break;
+        if (fabs(Bm) > (R)1e150) {
+            const R s = 1 / Bm;
+            Am *= s; Ap *= s; Bp *= s; Bm = 1;
         }
     }
     return Am / Bm;
 }
 
 // log F_nu(t) and log pdf_nu(t) for t <= 0.
-__host__ __device__ inline void t_lower_logs(const TConst& k, double t, double* lnF, double* lpdf) {
-    const double at = fabs(t);
-    double L;                                   // log(nu + t^2)
-    double ln_t2;                               // log(t^2)
-    if (at > 1e100) {
-        const double la = log(at);
-        ln_t2 = 2.0 * la;
-        L = ln_t2 + log1p((k.nu / at) / at);
+template <class R = double>
+__host__ __device__ inline void t_lower_logs(const TConst& k, R t, R* lnF, R* lpdf) {
+    const R nu = k.nu, at = fabs(t);
+    R L;                                        // log(nu + t^2)
+    R ln_t2;                                    // log(t^2)
+    if (at > (R)1e100) {
+        const R la = log(at);
+        ln_t2 = 2 * la;
+        L = ln_t2 + log1p((nu / at) / at);
     } else {
-        const double t2 = at * at;
+        const R t2 = at * at;
         ln_t2 = log(t2);
-        L = log(k.nu + t2);
+        L = log(nu + t2);
     }
-    *lpdf = k.ln_k - 0.5 * (k.nu + 1.0) * (L - k.ln_nu);
-    const double lnx = k.ln_nu - L;             // x = nu / (nu + t^2)
-    const double x = exp(lnx);
-    if (x < k.split) {
+    *lpdf = (R)k.ln_k - (R)0.5 * (nu + 1) * (L - (R)k.ln_nu);
+    const R lnx = (R)k.ln_nu - L;               // x = nu / (nu + t^2)
+    const R x = exp(lnx);
+    if (x < (R)k.split) {
         // F = 0.5 * I_x(a, 1/2) = 0.5 * x^a (1-x)^(1/2) / (a B) * cf
-        const double ln1mx = ln_t2 - L;
-        *lnF = -0.69314718055994530942 + k.a * lnx + 0.5 * ln1mx - k.lbeta - k.ln_a +
-               log(ibeta_cf(k.cf_dir, k.cf_terms, x));
+        const R ln1mx = ln_t2 - L;
+        *lnF = (R)-0.693147180559945309417232121458176568L + (R)k.a * lnx + (R)0.5 * ln1mx - (R)k.lbeta -
+               (R)k.ln_a + log(ibeta_cf<R>(k.cf_dir, k.cf_terms, x));
     } else {
         // F = 0.5 * (1 - I_y(1/2, a)),  y = t^2 / (nu + t^2) small
-        const double y = (at * at) / (k.nu + at * at);
-        double front = 0.0;
-        if (y > 0.0) front = exp(0.5 * log(y) + k.a * log1p(-y) - k.lbeta) * 2.0 * ibeta_cf(k.cf_cmp, k.cf_terms, y);
-        *lnF = log(0.5 * (1.0 - front));
+        const R y = (at * at) / (nu + at * at);
+        R front = 0;
+        if (y > 0) front = exp((R)0.5 * log(y) + (R)k.a * log1p(-y) - (R)k.lbeta) * 2 * ibeta_cf<R>(k.cf_cmp, k.cf_terms, y);
+        *lnF = log((R)0.5 * (1 - front));
     }
 }
 
@@ -160,28 +172,30 @@ __host__ __device__ __forceinline__ double tppf_table_guess(const TConst& k, dou
 // Halley on g(t) = log F(t) - lp for t < 0 (cubic convergence; stop once a step
 // is below 1e-6 relative: the next error is then ~1e-18).  Bisection fallback
 // whenever a step leaves the bracket F(lo) < p < F(hi).
-__host__ __device__ inline double tppf_refine(const TConst& k, double t, double lp) {
-    const double nu = k.nu;
-    double lo = -pos_inf(), hi = 0.0;
+template <class R = double>
+__host__ __device__ inline R tppf_refine(const TConst& k, R t, R lp) {
+    constexpr R step_done = sizeof(R) > 8 ? (R)1e-7 : (R)1e-6;
+    const R nu = k.nu, inf = (R)pos_inf();
+    R lo = -inf, hi = 0;
     for (int it = 0; it < 60; ++it) {
-        double lnF, lpdf;
-        t_lower_logs(k, t, &lnF, &lpdf);
-        const double g = lnF - lp;
-        if (g > 0.0) hi = t; else lo = t;
-        if (g == 0.0) break;
-        const double h = exp(lpdf - lnF);                   // g'  = pdf / F
-        const double dl = -(nu + 1.0) * t / (nu + t * t);    // pdf'/pdf
-        const double gn = g / h;
-        const double den = 1.0 - 0.5 * gn * (dl - h);       // 1 - g g'' / (2 g'^2)
-        double tn = (den > 0.5 && den < 2.0) ? t - gn / den : t - gn;
+        R lnF, lpdf;
+        t_lower_logs<R>(k, t, &lnF, &lpdf);
+        const R g = lnF - lp;
+        if (g > 0) hi = t; else lo = t;
+        if (g == 0) break;
+        const R h = exp(lpdf - lnF);                        // g'  = pdf / F
+        const R dl = -(nu + 1) * t / (nu + t * t);           // pdf'/pdf
+        const R gn = g / h;
+        const R den = 1 - (R)0.5 * gn * (dl - h);            // 1 - g g'' / (2 g'^2)
+        R tn = (den > (R)0.5 && den < 2) ? t - gn / den : t - gn;
         if (tn == t) break;                                  // correction below one ulp
         bool fallback = false;
         if (!(tn >= lo && tn <= hi)) {                        // outside the bracket: bisect
             fallback = true;
-            if (lo == -pos_inf()) tn = 2.0 * t - 1.0;
-            else tn = 0.5 * (lo + hi);
+            if (lo == -inf) tn = 2 * t - 1;
+            else tn = (R)0.5 * (lo + hi);
         }
-        const bool done = !fallback && fabs(tn - t) <= 1e-6 * fabs(tn);
+        const bool done = !fallback && fabs(tn - t) <= step_done * fabs(tn);
         t = tn;
         if (done) break;
     }
@@ -190,10 +204,30 @@ __host__ __device__ inline double tppf_refine(const TConst& k, double t, double 
 
 // Power-tail guess for log p = lp: F = exp(ln_tail)|t|^-nu (1 - A / t^2 + ...),
 // A = nu^2 (nu+1) / (2 (nu+2)), inverted to first order: t0 (1 - A / (nu t0^2)).
-__host__ __device__ __forceinline__ double tppf_tail_guess(const TConst& k, double lp) {
-    const double nu = k.nu;
-    double t = -exp((k.ln_tail - lp) / nu);
-    return t * (1.0 - nu * (nu + 1.0) / (2.0 * (nu + 2.0) * t * t));
+template <class R = double>
+__host__ __device__ __forceinline__ R tppf_tail_guess(const TConst& k, R lp) {
+    const R nu = k.nu;
+    R t = -exp(((R)k.ln_tail - lp) / nu);
+    return t * (1 - nu * (nu + 1) / (2 * (nu + 2) * t * t));
+}
+
+__host__ __device__ __forceinline__ double quintic(const double* __restrict__ tab, int n, double x) {
+    int k = (int)x;
+    k = k < 0 ? 0 : (k > n - 1 ? n - 1 : k);
+    const double s = x - k;
+    const double* c = tab + 6 * k;
+    return fma(fma(fma(fma(fma(c[5], s, c[4]), s, c[3]), s, c[2]), s, c[1]), s, c[0]);
+}
+
+// t.ppf at pp in (0, 1/2) straight from the plan's degree-5 tables (see
+// build_tppf_quintic): centre t = d r(d), d = 1/2 - pp; tail t = -1 / (v q(v)).
+__host__ __device__ __forceinline__ double tppf_quintic(const TConst& k, double pp) {
+    if (pp >= k.p_split) {
+        const double d = 0.5 - pp;
+        return d * quintic(k.q_c, k.n_qc, d * k.inv_qc);
+    }
+    const double v = exp(log(pp) * k.inv_nu);
+    return -1.0 / (v * quintic(k.q_v, k.n_qv, v * k.inv_qv));
 }
 
 // Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
@@ -204,8 +238,12 @@ __host__ __device__ inline double stdtrit(const TConst& k, double p) {
     if (p == 0.5) return 0.0;
     const bool upper = p > 0.5;
     const double pp = upper ? (1.0 - p) : p;   // exact
+    if (k.q_c != nullptr) {                    // the plan's verified direct tables
+        const double t = tppf_quintic(k, pp);
+        return upper ? -t : t;
+    }
     const double nu = k.nu;
-    double t = tppf_table_guess(k, pp);        // the plan's tables: one Halley step
+    double t = tppf_table_guess(k, pp);        // the plan's cubic tables: one Halley step
     if (!(t < 0.0)) {
         // Cornish-Fisher around the normal quantile, or the power tail.
         const double z = ndtri_approx(pp);

@@ -23,11 +23,17 @@ int main(int argc, char** argv) {
     bool ok = false;
     int nc = 256, nv = 64;
     for (; nc <= 4096 && !ok; nc *= 2, nv *= 2) ok = build_tppf_tables(k, nc, nv, tab);
-    fprintf(stderr, "tables ok=%d n_c=%d n_v=%d\n", ok, k.n_c, k.n_v);
     if (!ok) k.tab_c = nullptr;
+    std::vector<double> quint;
+    bool qok = false;
+    if (ok)
+        for (int qc = 256; qc <= 4096 && !qok; qc *= 2) qok = build_tppf_quintic(k, qc, qc < 1024 ? 128 : qc / 4, quint);
+    fprintf(stderr, "tables ok=%d n_c=%d n_v=%d quintic ok=%d n_qc=%d n_qv=%d\n", ok, k.n_c, k.n_v, qok, k.n_qc, k.n_qv);
+    TConst kq = k;
+    if (qok) { kq.q_c = quint.data(); kq.q_v = quint.data() + 6 * k.n_qc; }
     double p;
     while (scanf("%lf", &p) == 1) {
         TConst plain = k; plain.tab_c = nullptr;
-        printf("%.17g %.17g %.17g\n", stdtrit(k, p), tppf_table_guess(k, p < 0.5 ? p : 1 - p), stdtrit(plain, p));
+        printf("%.17g %.17g %.17g\n", stdtrit(kq, p), tppf_table_guess(k, p < 0.5 ? p : 1 - p), stdtrit(plain, p));
     }
 }
