@@ -53,9 +53,12 @@ __device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
 #ifndef CVQ_DIRECT_ILP
 #define CVQ_DIRECT_ILP 2
 #endif
-template <int COP, bool MSM, int QT, int RPT, int PM, int ILP = CVQ_DIRECT_ILP>
-__global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, const double* __restrict__ tA,
-                                                        const double* __restrict__ tB, const double* __restrict__ pi,
+// FUSED: evaluate the date's tables here (table_entry; Student only with the
+// plan's direct t.ppf tables); else read k_tables' output tA / tB [T][2][n].
+template <int COP, bool MSM, int QT, int RPT, int PM, bool FUSED, int ILP = CVQ_DIRECT_ILP>
+__global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, const double* __restrict__ a,
+                                                        const double* __restrict__ tA, const double* __restrict__ tB,
+                                                        const double* __restrict__ pi,
                                                         int mode, const double* __restrict__ bounds,
                                                         double* __restrict__ out, double* __restrict__ snaps,
                                                         Header* hdr) {
@@ -79,18 +82,24 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         if (stamps && tid == 0) stamps[idx] = __builtin_amdgcn_s_memtime();
     };
     stamp(0);
-    const double* At = tA + t * 2 * n;              // k_tables output [T][2][n]
-    const double* Bt = tB + t * 2 * n;
     // Student + MSM folds every per-node factor that is constant along a row or a
     // column: node = b^-(nu+2)/2 * sum_b G'_b[r] F'_b[j] with F' = F * B_col and
     // G' = G * term1 * B_row, and b = 1 + q/nu = R_r + z_j (P_r + C z_j).  A non-
     // finite z makes b non-finite (pow -> 0) and its B infinite, so the node is
     // 0 * inf = NaN exactly where student.py's 0/0 gives NaN (Q15, no guard on MSM).
+    // This date's marginal / quantile tables (k_tables' table_entry, evaluated
+    // here): axis 1 -> LDS column records, axis 0 -> this thread's row constants.
     for (int i = tid; i < n; i += NT) {
         sx[i] = S.x[i];
         double* c = col + i * CS;
-        c[0] = At[n + i];
-        const double Bc = Bt[n + i];
+        double Ac, Bc;
+        if constexpr (FUSED) {
+            table_entry<COP, MSM, COP == CVQ_STUDENT>(S, a, t * 2 + 1, 1, i, &Ac, &Bc);
+        } else {
+            Ac = tA[(t * 2 + 1) * n + i];
+            Bc = tB[(t * 2 + 1) * n + i];
+        }
+        c[0] = Ac;
 #pragma unroll
         for (int b = 0; b < QT; ++b) {
             const double f = S.F[((size_t)QT + b) * n + i];
@@ -110,7 +119,14 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         const int r = slot + 256 * k;
         has[k] = r < n;
         const int rr = has[k] ? r : 0;
-        ctx[k] = make_row<COP, 2>(S, At[rr], 0.0, Bt[rr]);
+        double Ar, Br;
+        if constexpr (FUSED) {
+            table_entry<COP, MSM, COP == CVQ_STUDENT>(S, a, t * 2, 0, rr, &Ar, &Br);
+        } else {
+            Ar = tA[t * 2 * n + rr];
+            Br = tB[t * 2 * n + rr];
+        }
+        ctx[k] = make_row<COP, 2>(S, Ar, 0.0, Br);
         lev[k] = S.x[rr] * S.w1;                      // integration_algo.py:20 (2-D)
         const double z0 = ctx[k].z0;
         Rr[k] = fma(S.Ri[0] * S.inv_nu, z0 * z0, 1.0);
@@ -320,11 +336,15 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         if (!((nz >> k) & 1ull)) { kstop = k; break; }
     for (long long d = tid; d < (long long)gridDim.x; d += NT)
         P.fin_var[d] = snaps[d * P.stride + kstop] + P.ptf_mean;
+    __syncthreads();                                     // every thread has read the header
     if (tid == 0) {
         P.fin_err[0] = e;
         P.fin_err[1] = kstop;
         P.fin_err[2] = N;
         P.fin_err[3] = 0;                                // ticket reset for the next launch
+        hdr->iters = 0;                                  // header reset for the next launch
+        hdr->error = 0;
+        hdr->nonzero = 0;
     }
 }
 

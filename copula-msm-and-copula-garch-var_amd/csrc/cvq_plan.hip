@@ -246,6 +246,10 @@ void launch_slab_t(cvq_plan* p, const double* bounds, double* out) {
 }
 
 // ---------------------------------------------------------------- DIRECT
+// k_direct computes its own tables unless the plan is Student without direct
+// t.ppf tables (then k_tables runs first and k_direct reads tA / tB).
+bool direct_fused(const cvq_plan* p) { return p->S.copula != CVQ_STUDENT || p->S.tk.q_c != nullptr; }
+
 template <int COP, bool MSM, int QT, int PM>
 void launch_direct_qp(cvq_plan* p, const SolveConst& P, int mode, const double* bounds, double* out, double* snaps,
                       Header* hdr) {
@@ -253,12 +257,13 @@ void launch_direct_qp(cvq_plan* p, const SolveConst& P, int mode, const double* 
     constexpr bool fold = (COP == CVQ_STUDENT) && MSM;
     constexpr int cs = ((1 + QT + (fold ? 0 : 1)) + 1) & ~1;      // k_direct's column record
     const size_t lds = sizeof(double) * ((size_t)(cs + 1) * p->S.n + 8);
-    if (rpt == 1)
-        hipLaunchKernelGGL((k_direct<COP, MSM, QT, 1, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr);
-    else
-        hipLaunchKernelGGL((k_direct<COP, MSM, QT, 2, PM>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P,
-                           p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr);
+#define CVQ_DIRECT_LAUNCH(R, FU)                                                                                   \
+    hipLaunchKernelGGL((k_direct<COP, MSM, QT, R, PM, FU>), dim3((unsigned)p->T), dim3(256), lds, p->stream, p->S, P, \
+                       p->in_a, p->d_tA, p->d_tB, p->in_pi, mode, bounds, out, snaps, hdr)
+    const bool fused = direct_fused(p);
+    if (rpt == 1) { if (fused) CVQ_DIRECT_LAUNCH(1, true); else CVQ_DIRECT_LAUNCH(1, false); }
+    else { if (fused) CVQ_DIRECT_LAUNCH(2, true); else CVQ_DIRECT_LAUNCH(2, false); }
+#undef CVQ_DIRECT_LAUNCH
 }
 
 template <int COP, bool MSM, int QT>
@@ -410,6 +415,10 @@ int dispatch_cop(cvq_plan* p, bool tables) {
 int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
+    if (p->strategy == CVQ_STRATEGY_DIRECT && direct_fused(p)) {   // k_direct evaluates its own tables
+        if (hdr) CVQ_HIP_CHECK(hipMemsetAsync(hdr, 0, sizeof(Header), p->stream));
+        return CVQ_OK;
+    }
     if (!p->tables_valid) {
         TimedScope ts(p, TK_TABLES);
         p->zero_hdr = hdr;
@@ -635,6 +644,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     p->stream = p->own_stream;
     e = hipMemset(p->d_err, 0, 4 * sizeof(int));         // error words + the fused-finalize ticket
+    if (e == hipSuccess) e = hipMemset(p->d_hdr, 0, sizeof(Header));
     if (e == hipSuccess) e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_kmax, kmax.data(), kmax.size() * sizeof(int), hipMemcpyHostToDevice);
@@ -736,7 +746,9 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
     if (realloc) {
         int rc;
         if ((rc = dev_alloc(&p->d_a, na)) || (rc = dev_alloc(&p->d_pi, npi))) return rc;
-        if ((rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) || (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n)))
+        const bool tables = p->strategy == CVQ_STRATEGY_PREFIX || !direct_fused(p);
+        if (tables && ((rc = dev_alloc(&p->d_tA, (size_t)T * S.dim * S.n)) ||
+                       (rc = dev_alloc(&p->d_tB, (size_t)T * S.dim * S.n))))
             return rc;
         if (p->strategy == CVQ_STRATEGY_PREFIX && (rc = dev_alloc(&p->d_C, (size_t)T * S.G))) return rc;
         p->capT = T;
@@ -825,7 +837,8 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;
-    if ((rc = ensure_mass(p, p->d_hdr))) return rc;
+    // DIRECT keeps p->d_hdr zero itself (zeroed at creation, reset by the fused finalize)
+    if ((rc = ensure_mass(p, p->strategy == CVQ_STRATEGY_DIRECT ? nullptr : p->d_hdr))) return rc;
     bool exact;
     int K = bisect_budget(*a, &exact);
     if (!exact) K += 2;

@@ -70,7 +70,8 @@ __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __res
 //   A   = z = t.ppf(u, nu) | norm.ppf(u)        (Plackett: A = u)
 //   B   = pdf / univariate-copula-margin-pdf      (MSM: pdf = 1; Plackett: B = pdf)
 // Layout [T][dim][n], coalesced along i.
-template <int COP, bool MSM>
+// TAB: the plan has verified direct t.ppf tables (Student only; see stdtrit_tabulated).
+template <int COP, bool MSM, bool TAB = false>
 __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __restrict__ a, long long td, int d,
                                             int i, double* A_out, double* B_out) {
     double u, pdf = 1.0;
@@ -92,7 +93,7 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
     } else {
         double z, uni;
         if (COP == CVQ_STUDENT) {
-            z = stdtrit(S.tk, u);                                // student.py:102
+            z = TAB ? stdtrit_tabulated(S.tk, u) : stdtrit(S.tk, u);   // student.py:102
             uni = isfinite(z) ? S.g_uni * pow_half_neg(1.0 + (z * z) / S.nu, S.uni_m, S.uni_ex) : 0.0;   // :164-172
         } else {
             z = ndtri(u);                                        // gaussian.py:44

@@ -230,18 +230,9 @@ __host__ __device__ __forceinline__ double tppf_quintic(const TConst& k, double 
     return -1.0 / (v * quintic(k.q_v, k.n_qv, v * k.inv_qv));
 }
 
-// Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
-__host__ __device__ inline double stdtrit(const TConst& k, double p) {
-    if (!(p >= 0.0 && p <= 1.0) || !(k.nu > 0.0)) return __builtin_nan("");
-    if (p == 0.0) return -pos_inf();
-    if (p == 1.0) return pos_inf();
-    if (p == 0.5) return 0.0;
-    const bool upper = p > 0.5;
-    const double pp = upper ? (1.0 - p) : p;   // exact
-    if (k.q_c != nullptr) {                    // the plan's verified direct tables
-        const double t = tppf_quintic(k, pp);
-        return upper ? -t : t;
-    }
+// t.ppf for pp in (0, 1/2) without the direct tables: Cornish-Fisher / power-tail
+// or cubic-table guess, then Halley.
+__host__ __device__ inline double tppf_lower_refined(const TConst& k, double pp) {
     const double nu = k.nu;
     double t = tppf_table_guess(k, pp);        // the plan's cubic tables: one Halley step
     if (!(t < 0.0)) {
@@ -251,12 +242,36 @@ __host__ __device__ inline double stdtrit(const TConst& k, double p) {
         const double tcf = z + (z2 * z + z) / (4.0 * nu) +
                            (((5.0 * z2 + 16.0) * z2 + 3.0) * z) / (96.0 * nu * nu) +
                            ((((3.0 * z2 + 19.0) * z2 + 17.0) * z2 - 15.0) * z) / (384.0 * nu * nu * nu);
-        if (nu > 1e5) return upper ? -tcf : tcf;
+        if (nu > 1e5) return tcf;
         const double ttail = tppf_tail_guess(k, log(pp));
         t = (ttail < tcf && z2 > nu) ? ttail : tcf;
         if (!(t < 0.0)) t = -1e-3;
     }
-    t = tppf_refine(k, t, log(pp));
+    return tppf_refine(k, t, log(pp));
+}
+
+// stdtrit for plans whose direct tables exist (k.q_c != nullptr): no refinement
+// code at all, so kernels that inline it keep a small register budget.
+__host__ __device__ __forceinline__ double stdtrit_tabulated(const TConst& k, double p) {
+    if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
+    if (p == 0.0) return -pos_inf();
+    if (p == 1.0) return pos_inf();
+    if (p == 0.5) return 0.0;
+    const bool upper = p > 0.5;
+    const double t = tppf_quintic(k, upper ? (1.0 - p) : p);
+    return upper ? -t : t;
+}
+
+// Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
+__host__ __device__ inline double stdtrit(const TConst& k, double p) {
+    if (!(p >= 0.0 && p <= 1.0) || !(k.nu > 0.0)) return __builtin_nan("");
+    if (p == 0.0) return -pos_inf();
+    if (p == 1.0) return pos_inf();
+    if (p == 0.5) return 0.0;
+    const bool upper = p > 0.5;
+    const double pp = upper ? (1.0 - p) : p;   // exact
+    const double t = (k.q_c != nullptr) ? tppf_quintic(k, pp)      // the plan's verified direct tables
+                                        : tppf_lower_refined(k, pp);
     return upper ? -t : t;
 }
 
