@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
-    ap.add_argument("--strategy", default="direct", choices=["prefix", "direct"])
+    ap.add_argument("--strategy", default="direct", choices=["prefix", "direct", "binned"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
     ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
     ap.add_argument("--cpu-jobs", type=int, default=0)

@@ -14,6 +14,7 @@
 #include "cvq_common.h"
 #include "cvq_quad_kernels.h"
 #include "cvq_direct_kernels.h"
+#include "cvq_binned_kernels.h"
 #include "cvq_tppf_tables.h"
 
 namespace cvq {
@@ -143,6 +144,11 @@ struct cvq_plan {
     long long capIO = 0;
     double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
     unsigned long long* d_stamps = nullptr;   // diagnostic phase stamps (CVQ_STAMPS=1)
+    // BINNED: host grid copy + date-independent cut tables for the cached solve arguments
+    std::vector<double> hx;
+    int16_t* d_cut = nullptr;    // cut1 [n][kE1+1] then cutB [3][n][kBins+1]
+    double bin_key[6] = {0, 0, 0, 0, 0, 0};
+    bool bin_valid = false;
     long long capStamps = 0;
     // optional per-kernel timing (HIP events on the plan's stream)
     int timing = 0;              // bitmask of kernel kinds timed with HIP events
@@ -303,19 +309,105 @@ int launch_direct(cvq_plan* p, const SolveConst& P, int mode, const double* boun
     return CVQ_OK;
 }
 
+int ensure_stamps(cvq_plan* p) {
+    if (p->T > p->capStamps) {
+        if (p->d_stamps) (void)hipFree(p->d_stamps);
+        p->d_stamps = nullptr;
+        p->capStamps = 0;
+        CVQ_HIP_CHECK(hipMalloc((void**)&p->d_stamps, (size_t)p->T * 32 * 8));
+        p->capStamps = p->T;
+    }
+    return CVQ_OK;
+}
+
+// ---------------------------------------------------------------- BINNED
+// Cut columns cnt_r(v) = largest j with x_j <= (v - x_r w1) / w0 (else 0), exactly
+// as the device's count_le over [0, n-1] (create_grids.py:104-108, Q9/Q10).
+int host_cnt(const std::vector<double>& x, double lev, double w0, double v) {
+    const double g = (v - lev) / w0;
+    int lo = 0, hi = (int)x.size() - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (x[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Edges of the depth-kBinLevels bisection tree of (lo, hi]: the midpoints
+// (lo + hi) / 2 the reference computes at every node (calc_var_class.py:279).
+void tree_edges(double lo, double hi, double* ed) {
+    ed[0] = lo;
+    ed[kBins] = hi;
+    for (int s = kBins / 2; s >= 1; s >>= 1)
+        for (int e = s; e < kBins; e += 2 * s) ed[e] = (ed[e - s] + ed[e + s]) / 2;
+}
+
+// 0: cut tables ready for these arguments; 1: arguments outside the binned
+// layout (lower < sg0 < fg < sg1 < vmax, vmin < sg0 required); <0: error.
+int ensure_bingeom(cvq_plan* p, const SolveConst& P) {
+    const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
+    if (!(P.lower < P.sg0 && P.sg0 < P.fg && P.fg < P.sg1 && P.sg1 < P.vmax && P.vmin < P.sg0)) return 1;
+    if (p->bin_valid && std::memcmp(key, p->bin_key, sizeof key) == 0) return 0;
+    const int n = p->S.n;
+    const size_t n1 = (size_t)n * (kE1 + 1), nb = (size_t)3 * n * (kBins + 1);
+    std::vector<int16_t> h(n1 + nb);
+    double ed[kBins + 1];
+    tree_edges(P.sg1, P.vmax, ed);
+    for (int r = 0; r < n; ++r) {
+        const double lev = p->hx[r] * p->S.w1;                 // integration_algo.py:20 (2-D)
+        int16_t* c = h.data() + (size_t)r * (kE1 + 1);
+        c[0] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.lower);
+        c[1] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.sg0);
+        c[2] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.fg);
+        for (int e = 0; e <= kBins; ++e) c[3 + e] = (int16_t)host_cnt(p->hx, lev, p->S.w0, ed[e]);
+    }
+    const double br[3][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.fg, P.sg1}};
+    for (int b = 0; b < 3; ++b) {
+        tree_edges(br[b][0], br[b][1], ed);
+        for (int r = 0; r < n; ++r) {
+            const double lev = p->hx[r] * p->S.w1;
+            int16_t* c = h.data() + n1 + ((size_t)b * n + r) * (kBins + 1);
+            for (int e = 0; e <= kBins; ++e) c[e] = (int16_t)host_cnt(p->hx, lev, p->S.w0, ed[e]);
+        }
+    }
+    p->bin_valid = false;
+    if (!p->d_cut) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cut, h.size() * sizeof(int16_t)));
+    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cut, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    std::memcpy(p->bin_key, key, sizeof key);
+    p->bin_valid = true;
+    return 0;
+}
+
+}  // namespace
+namespace cvq {
+int launch_binned(const StaticDev& S, const SolveConst& P, const BinGeom& BG, long long T, hipStream_t stream,
+                  const double* a, const double* pi, double* st, double* snaps, Header* hdr);   // cvq_binned.hip
+}
+namespace {
+
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
-    if (p->strategy == CVQ_STRATEGY_DIRECT) {
+    if (p->strategy == CVQ_STRATEGY_BINNED && direct_fused(p)) {
+        int rc = ensure_bingeom(p, P);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+            static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
+            double* st = nullptr;
+            if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
+            if (dbg_stamps) st = (double*)p->d_stamps;
+            const BinGeom BG{p->d_cut, p->d_cut + (size_t)p->S.n * (kE1 + 1)};
+            return launch_binned(p->S, P, BG, p->T, p->stream, p->in_a, p->in_pi, st, snaps, hdr);
+        }
+        // rc > 0: solve arguments outside the binned layout -> slab-by-slab k_direct
+    }
+    if (p->strategy != CVQ_STRATEGY_PREFIX) {
         // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
         static const int dbg_mode = getenv("CVQ_DIRECT_ABLATE") ? atoi(getenv("CVQ_DIRECT_ABLATE")) : 0;
         static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
         double* st = nullptr;
         if (dbg_stamps) {
-            if (p->T > p->capStamps) {
-                if (p->d_stamps) (void)hipFree(p->d_stamps);
-                if (hipMalloc((void**)&p->d_stamps, (size_t)p->T * 32 * 8) != hipSuccess) p->d_stamps = nullptr;
-                p->capStamps = p->d_stamps ? p->T : 0;
-            }
+            if (int rc = ensure_stamps(p)) return rc;
             st = (double*)p->d_stamps;
         }
         return launch_direct(p, P, dbg_mode == 2 ? 2 : 0, nullptr, st, snaps, hdr);
@@ -335,7 +427,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     TimedScope ts(p, TK_SLAB);
-    if (p->strategy == CVQ_STRATEGY_DIRECT) {
+    if (p->strategy != CVQ_STRATEGY_PREFIX) {      // BINNED: slabs of arbitrary bounds run k_direct
         SolveConst P{};
         return launch_direct(p, P, 1, bounds, out, nullptr, nullptr);
     }
@@ -415,7 +507,7 @@ int dispatch_cop(cvq_plan* p, bool tables) {
 int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
-    if (p->strategy == CVQ_STRATEGY_DIRECT && direct_fused(p)) {   // k_direct evaluates its own tables
+    if (p->strategy != CVQ_STRATEGY_PREFIX && direct_fused(p)) {   // k_direct / k_binned evaluate their tables
         if (hdr) CVQ_HIP_CHECK(hipMemsetAsync(hdr, 0, sizeof(Header), p->stream));
         return CVQ_OK;
     }
@@ -461,7 +553,7 @@ int check_args(const cvq_plan* p, const cvq_solve_args* a) {
     CVQ_REQUIRE(a != nullptr, CVQ_ERR_INVALID, "solve args is NULL");
     const double top = std::max({a->first_guess, a->second_guess_lo, a->second_guess_hi, a->max_var, a->min_var,
                                  a->lower});
-    CVQ_REQUIRE(p->strategy == CVQ_STRATEGY_DIRECT || !(top > p->v_cap), CVQ_ERR_RANGE,
+    CVQ_REQUIRE(p->strategy != CVQ_STRATEGY_PREFIX || !(top > p->v_cap), CVQ_ERR_RANGE,
                 "a VaR level in the solve arguments exceeds the plan's v_cap");
     CVQ_REQUIRE(a->tolerance > 0.0, CVQ_ERR_INVALID, "tolerance must be > 0");
     return CVQ_OK;
@@ -536,10 +628,10 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
                 CVQ_ERR_INVALID, "NULL static table");
     CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
     CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
-    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX || s->strategy == CVQ_STRATEGY_DIRECT, CVQ_ERR_INVALID,
-                "unknown strategy");
-    CVQ_REQUIRE(!(s->strategy == CVQ_STRATEGY_DIRECT && s->dim != 2), CVQ_ERR_UNSUPPORTED,
-                "the DIRECT strategy is built for dim == 2");
+    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX || s->strategy == CVQ_STRATEGY_DIRECT ||
+                    s->strategy == CVQ_STRATEGY_BINNED, CVQ_ERR_INVALID, "unknown strategy");
+    CVQ_REQUIRE(!(s->strategy != CVQ_STRATEGY_PREFIX && s->dim != 2), CVQ_ERR_UNSUPPORTED,
+                "the DIRECT and BINNED strategies are built for dim == 2");
     for (int l = 0; l < Q; ++l) {             // create_vol_combinations ij order (msm_estimation.py:384)
         int rem = l;
         for (int d = s->dim - 1; d >= 0; --d) {
@@ -557,6 +649,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     p->device = device;
     p->strategy = s->strategy;
     p->v_cap = s->v_cap;
+    p->hx.assign(s->x_values, s->x_values + s->n);
     StaticDev& S = p->S;
     S.model = s->model;
     S.copula = s->copula;
@@ -679,7 +772,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
-                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps})
+                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps, (void*)p->d_cut})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
@@ -837,8 +930,8 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;
-    // DIRECT keeps p->d_hdr zero itself (zeroed at creation, reset by the fused finalize)
-    if ((rc = ensure_mass(p, p->strategy == CVQ_STRATEGY_DIRECT ? nullptr : p->d_hdr))) return rc;
+    // DIRECT / BINNED keep p->d_hdr zero themselves (zeroed at creation, reset by the fused finalize)
+    if ((rc = ensure_mass(p, p->strategy != CVQ_STRATEGY_PREFIX ? nullptr : p->d_hdr))) return rc;
     bool exact;
     int K = bisect_budget(*a, &exact);
     if (!exact) K += 2;
@@ -853,12 +946,12 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
         }
         if (!first) CVQ_HIP_CHECK(hipMemsetAsync(p->d_hdr, 0, sizeof(Header), p->stream));
         SolveConst P = solve_const(*a, K);
-        if (p->strategy == CVQ_STRATEGY_DIRECT) {       // finalize fused into the solve's last workgroup
+        if (p->strategy != CVQ_STRATEGY_PREFIX) {       // finalize fused into the solve's last workgroup
             P.fin_var = d_var;
             P.fin_err = p->d_err;
         }
         if ((rc = launch_solve(p, P, p->d_snap, p->d_hdr))) return rc;
-        if (p->strategy != CVQ_STRATEGY_DIRECT) {
+        if (p->strategy == CVQ_STRATEGY_PREFIX) {
             const unsigned blocks = (unsigned)((p->T + 255) / 256);
             TimedScope ts(p, TK_FINALIZE);
             hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(256), 0, p->stream, (const Header*)p->d_hdr, 1,

@@ -54,6 +54,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // -------------------------------------------------------- static Phi (MSM only)
 // phi[d][s][i] = 0.5 * (1 + erf((x_i / sigma_{d,s}) / sqrt 2))  (msm_integration_function.py:32-36)
+#ifndef CVQ_NO_PLAN_KERNELS    // non-template kernels live in cvq_plan.hip only
 __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __restrict__ phi) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = S.dim * S.q * S.n;
@@ -63,6 +64,7 @@ __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __res
     const double xs = S.x[i] / uvs[ds];
     phi[idx] = 0.5 * (1.0 + erf(xs / kInvSqrt2));
 }
+#endif
 
 // ---------------------------------------------------------------- k_tables
 // One thread per (date t, axis d, grid index i):
@@ -481,6 +483,7 @@ __global__ __launch_bounds__(TPD) void k_slab_prefix(StaticDev S, const double* 
 
 // Finalise: combine rank headers (Q2 global iteration count, Q4 global break)
 // and pick each date's snapshot; var = mid + ptf_mean (calc_var_class.py:171).
+#ifndef CVQ_NO_PLAN_KERNELS
 __global__ void k_finalize(const Header* __restrict__ hdrs, int nranks, const double* __restrict__ snaps,
                            long long T_total, int stride, int K, double ptf_mean, double* __restrict__ var,
                            int* __restrict__ err) {
@@ -500,5 +503,6 @@ __global__ void k_finalize(const Header* __restrict__ hdrs, int nranks, const do
     if (t >= T_total) return;
     var[t] = snaps[t * stride + kstop] + ptf_mean;
 }
+#endif
 
 }  // namespace cvq
