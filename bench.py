@@ -11,8 +11,8 @@ after which every rank finalises the full VaR vector).
 One "step" = the calc_var-equivalent scope (utils/calc_var_class.py:95-177) over
 the batch, with the per-date forecast tables already resident in HBM:
   set per-date inputs (device copy) -> marginal/special-function tables (k_tables)
-  -> per-date slab-on-the-fly bisection solve (k_direct; DIRECT strategy, the
-  default) -> [all-gather] -> finalise (k_finalize).
+  -> per-date slab-on-the-fly bisection solve (k_compact; COMPACT strategy, the
+  default; --strategy direct: k_direct) -> [all-gather] -> finalise.
   (--strategy prefix: k_tables -> joint-mass row prefixes k_mass -> k_solve_prefix.)
 
 Prints ONE JSON line (rank 0).  Extra objects:
@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
-    ap.add_argument("--strategy", default="direct", choices=["prefix", "direct", "binned"])
+    ap.add_argument("--strategy", default="compact", choices=["prefix", "direct", "compact"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
     ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
@@ -186,8 +186,9 @@ def main():
                        "strategy": a.strategy},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_mass (joint-mass row prefix)" if dom == "mass"
-                                   else "k_direct (per-date slab-on-the-fly solve)",
+                         "kernel": {"prefix": "k_mass (joint-mass row prefix)",
+                                    "direct": "k_direct (per-date slab-on-the-fly solve)",
+                                    "compact": "k_compact (per-date solve, one-wave tail)"}[a.strategy],
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_us": dom_avg_s * 1e6,
                          "reach_nodes_per_date": plan.reach_nodes,
                          "fp64": {"achieved_tflops": fp64_tflops, "peak_tflops": FP64_PEAK_TFLOPS,

@@ -60,10 +60,10 @@ class QuadraturePlan:
         st.vol_states = dp(self._vs) if self._vs is not None else None
         st.copula_params = dp(self._cp)
         st.n_copula_params = self._cp.size
-        if strategy == "auto":                          # DIRECT / BINNED are built for 2 assets
-            strategy = "direct" if self.dim == 2 else "prefix"
+        if strategy == "auto":                          # DIRECT / COMPACT are built for 2 assets
+            strategy = "compact" if self.dim == 2 else "prefix"
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
-                       "binned": N.STRATEGY_BINNED}[strategy]
+                       "compact": N.STRATEGY_COMPACT}[strategy]
         self.strategy = strategy
         st.v_cap = float(v_cap)
         self._static = st

@@ -58,7 +58,7 @@ class ValueAtRiskCalcualtion:
         self.integrated_function = VaRCalculationMethod.integrated_function
 
         if strategy == "auto":
-            strategy = "direct" if self.dim == 2 else "prefix"
+            strategy = "compact" if self.dim == 2 else "prefix"
         densities, x_values, step_size, combos = self.grids_generations_params
         self.plan = QuadraturePlan(VaRCalculationMethod.model_kind, VaRCalculationMethod.copula_kind, self.dim,
                                    x_values, step_size, densities, combos, self.weights, self.copula_params,

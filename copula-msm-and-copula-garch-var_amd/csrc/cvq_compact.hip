@@ -1,0 +1,85 @@
+// cvq_compact.hip -- launch side of the COMPACT solve kernel (own translation
+// unit: its template instances compile in parallel with cvq_plan.hip).
+#include <hip/hip_runtime.h>
+
+#define CVQ_NO_PLAN_KERNELS
+
+#include "cvq_common.h"
+#include "cvq_compact_kernels.h"
+
+#ifndef CVQ_COMPACT_NT
+#define CVQ_COMPACT_NT 256
+#endif
+
+namespace cvq {
+namespace {
+
+struct CompactLaunch {
+    const StaticDev& S;
+    const SolveConst& P;
+    const CompactGeom& G;
+    long long T;
+    hipStream_t stream;
+    const double *a, *tA, *tB, *pi;
+    double *st, *snaps;
+    Header* hdr;
+    bool fused;
+};
+
+template <int COP, bool MSM, int PM, bool FUSED, int RPT>
+void launch_r(const CompactLaunch& L) {
+    constexpr int NT = CVQ_COMPACT_NT;
+    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED>), dim3((unsigned)L.T), dim3(NT),
+                       compact_lds_bytes(L.S.n, NT, L.G.nb), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st,
+                       L.snaps, L.hdr);
+}
+
+// rows per thread: ceil(n / NT) rounded up to 1, 2, 4 or 8 (n <= 8 NT)
+template <int COP, bool MSM, int PM, bool FUSED>
+void launch_f(const CompactLaunch& L) {
+    constexpr int NT = CVQ_COMPACT_NT;
+    const int rpt = (L.S.n + NT - 1) / NT;
+    if (rpt <= 1) launch_r<COP, MSM, PM, FUSED, 1>(L);
+    else if (rpt <= 2) launch_r<COP, MSM, PM, FUSED, 2>(L);
+    else if (rpt <= 4) launch_r<COP, MSM, PM, FUSED, 4>(L);
+    else launch_r<COP, MSM, PM, FUSED, 8>(L);
+}
+
+template <int COP, bool MSM, int PM>
+void launch_pm(const CompactLaunch& L) {
+    if (L.fused) launch_f<COP, MSM, PM, true>(L);
+    else launch_f<COP, MSM, PM, false>(L);
+}
+
+template <int COP, bool MSM>
+void launch_m(const CompactLaunch& L) {
+    if constexpr (COP == CVQ_STUDENT) {
+        if (L.S.node_m == 8) { launch_pm<COP, MSM, 8>(L); return; }      // nu = 6: b^-4, one rcp per node
+    }
+    launch_pm<COP, MSM, 0>(L);
+}
+
+template <int COP>
+void launch_c(const CompactLaunch& L) {
+    if (L.S.model == CVQ_MSM) launch_m<COP, true>(L);
+    else launch_m<COP, false>(L);
+}
+
+}  // namespace
+
+int compact_max_n() { return 8 * CVQ_COMPACT_NT; }
+
+int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
+                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
+                   double* snaps, Header* hdr) {
+    const CompactLaunch L{S, P, G, T, stream, a, tA, tB, pi, st, snaps, hdr, fused};
+    switch (S.copula) {
+        case CVQ_GAUSSIAN: launch_c<CVQ_GAUSSIAN>(L); break;
+        case CVQ_STUDENT: launch_c<CVQ_STUDENT>(L); break;
+        default: launch_c<CVQ_PLACKETT>(L); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+}  // namespace cvq

@@ -1,0 +1,623 @@
+// cvq_compact_kernels.h -- COMPACT strategy (2 assets): the DIRECT control flow
+// with a rank-1 node weight, one barrier per bisection level, O(1) grid lookups,
+// and the last bisection levels compacted into one wavefront.
+//
+// Reference: calc_var + bisection_algorithm (utils/calc_var_class.py:95-177,
+// :250-309) integrate 2 + K slabs (a, b] per date; a slab is, per outer row r,
+// the inner-index range (cnt_r(a), cnt_r(b)] with cnt_r(v) = largest j with
+// x_j <= (v - x_r w1) / w0, else 0 (create_grids.py:102-108, Q9/Q10).
+//
+// One NT-thread workgroup per date (NT = 64 by default: one wavefront, so the
+// per-level reductions need no LDS and no barrier); thread tid owns the outer
+// rows tid + NT k.
+//  1. Tables: thread i evaluates the table entries of grid index i on both axes
+//     (table_entry's arithmetic, the Student quantile written without
+//     data-dependent branches so the two entries' memory latencies overlap) ->
+//     LDS column records (z_j, B'_j) and LDS row records.
+//  2. r0, nr and the bracket take their per-row cuts from a date-independent
+//     table of the solve's fixed levels (lower, sg0, fg, sg1, vmin, vmax).
+//  3. Each bisection level: kM = cnt_r(mid) by a bucket lookup into the grid and
+//     an exact probe (count_le's result in O(1) LDS reads); the row owner sums
+//     its slab columns with kIlp independent node chains; ONE workgroup
+//     reduction returns (slab sum, slab nodes, bracket nodes).
+//  4. Tail: once the bracket holds <= kTailCap nodes, their (v*, value) pairs go
+//     to LDS -- v*(r, j) is the smallest level with node (r, j) inside, the exact
+//     FP64 membership rule, precomputed per plan -- and one wave runs the
+//     remaining levels alone with masked wave sums (no barriers, no searches).
+//
+// Phase stamps of the DIRECT kernel showed the per-level workgroup steps --
+// binary searches, reductions, barriers -- and the single-row critical paths,
+// not the node arithmetic, set a date's time; this kernel cuts each of them.
+//
+// Node values (fast path).  The MSM weight of node (r, j) is
+// sum_{a,b} pi[a][b] F0_a(r) F1_b(j) (msm_integration_function.py:45 with Q5's
+// rotation in F); the reference's pi is the outer product of the per-asset
+// forecasts (compute_forecast_combinations, msm_estimation.py:392-418), so W =
+// wr(r) wc(j), checked bitwise per date.  Then a node is
+// scale_r * f(row consts, z_j) * B'_j, B'_j = B_j wc(j):
+//   Student  f = (R_r + z (P_r + C z))^-(nu+2)/2   (student.py:133-141)
+//   Gaussian f = exp(-(R_r + z (P_r + Ri11 z)) / 2) (gaussian.py:105-113)
+//   Plackett f = (N_r + M_r v) / ((D_r + a1 v)(E_r - a1 v))^2   (plackett.py:66-69, Q11)
+// A date whose pi is not rank 1, or a GARCH/UKF date with a non-finite table
+// entry (nan_to_num semantics, garch_integration_function.py:45-50), takes the
+// generic per-node path (node_value, full W contraction) for the whole solve.
+#pragma once
+#include "cvq_direct_kernels.h"
+
+namespace cvq {
+
+#ifndef CVQ_TAIL_PER_LANE
+#define CVQ_TAIL_PER_LANE 4
+#endif
+constexpr int kTailPerLane = CVQ_TAIL_PER_LANE;     // tail nodes per lane of the tail wave
+constexpr int kTailCap = 64 * kTailPerLane;         // bracket size that switches to the tail
+constexpr int kRowRec = 8;                          // doubles per LDS row record
+constexpr int kColRec = 2;                          // doubles per LDS column record (16 B: lanes at
+                                                    // consecutive columns read conflict-free)
+constexpr int kCutFixed = 8;                        // int16 per row in the fixed-level cut table
+constexpr int kBucketsPerPoint = 4;                 // grid lookup buckets per grid point
+#ifndef CVQ_COMPACT_ILP
+#define CVQ_COMPACT_ILP 2
+#endif
+constexpr int kIlp = CVQ_COMPACT_ILP;               // independent node chains per row range
+
+// Fixed-level cut table columns: lower, sg0, fg, sg1, vmin, vmax (then padding).
+enum { kCutLower = 0, kCutSg0, kCutFg, kCutSg1, kCutVmin, kCutVmax };
+
+// Date-independent device tables of a COMPACT plan.
+struct CompactGeom {
+    const int16_t* cutfix;    // [n][kCutFixed] cut columns of the fixed levels (per solve arguments)
+    const double* vstar;      // [n][n] v*(r, j): smallest level with node (r, j) inside (Q9/Q10)
+    const int16_t* bucket;    // [nb] largest j with x_j <= bx0 + b / binv (0 if none): a start guess
+    double bx0, binv;         // bucket of a grid coordinate g: floor((g - bx0) * binv)
+    int nb;
+};
+
+// ------------------------------------------------------------------ reductions
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, true);
+}
+
+// Inclusive prefix sum over the 64 lanes: row_shr 1, 2, 4, 8 inside rows of 16,
+// then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += dpp_i32<0x111>(v);
+    v += dpp_i32<0x112>(v);
+    v += dpp_i32<0x114>(v);
+    v += dpp_i32<0x118>(v);
+    v += dpp_i32<0x142, 0xA>(v);
+    v += dpp_i32<0x143, 0xC>(v);
+    return v;
+}
+
+// Block-wide exclusive scan of v; *total = sum over the block.  One barrier.
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* wtot, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if constexpr (NT == 64) {
+        *total = __builtin_amdgcn_readlane(incl, 63);
+        return incl - v;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const int s = wtot[w];
+        base += (w < wave) ? s : 0;
+        tot += s;
+    }
+    *total = tot;
+    return base + incl - v;
+}
+
+// Workgroup sums of three values, identical in every thread (fixed order), one
+// barrier; red: 2 x 3 x NT / 64 doubles, parity alternates the half used.
+template <int NT>
+__device__ __forceinline__ void team_sum3(double a, double b, double c, double* red, int& parity, double* out) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    if constexpr (NT == 64) {                                   // one wave: no LDS, no barrier
+        out[0] = a;
+        out[1] = b;
+        out[2] = c;
+        return;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double* rr = red + parity * (3 * (NT / 64));
+    parity ^= 1;
+    if (lane == 0) {
+        rr[3 * wave] = a;
+        rr[3 * wave + 1] = b;
+        rr[3 * wave + 2] = c;
+    }
+    __syncthreads();
+    double s0 = rr[0], s1 = rr[1], s2 = rr[2];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) {
+        s0 += rr[3 * w];
+        s1 += rr[3 * w + 1];
+        s2 += rr[3 * w + 2];
+    }
+    out[0] = s0;
+    out[1] = s1;
+    out[2] = s2;
+}
+
+// count_le(sx, g, klo, khi) -- the largest j in [klo, khi] with x_j <= g, else klo
+// (x_klo <= g or klo == 0; create_grids.py:104-108) -- from a bucket guess and an
+// exact probe instead of a binary search.
+__device__ __forceinline__ int grid_count(const double* sx, const int16_t* bk, const CompactGeom& G, double g, int klo,
+                                          int khi) {
+    if (!(g == g) || khi <= klo) return klo;                    // NaN level: nothing is <= g
+    if (sx[khi] <= g) return khi;
+    const double fb = (g - G.bx0) * G.binv;
+    int j = fb < 0.0 ? 0 : (fb >= (double)(G.nb - 1) ? (int)bk[G.nb - 1] : (int)bk[(int)fb]);
+    j = min(max(j, klo), khi - 1);
+    while (j > klo && sx[j] > g) --j;
+    while (sx[j + 1] <= g) ++j;                                 // stops at khi - 1: x_khi > g
+    return j;
+}
+
+// ------------------------------------------------------------------ node values
+struct FastRow {
+    double c0, c1, c2, c3, scale;
+};
+
+template <int COP>
+__device__ __forceinline__ void fast_row_consts(const StaticDev& S, double z0, double B0, double wr, double* rec) {
+    if constexpr (COP == CVQ_STUDENT) {
+        rec[0] = fma(S.Ri[0] * S.inv_nu, z0 * z0, 1.0);                 // R_r  (k_direct's Rr)
+        rec[1] = (S.Ri[1] + S.Ri[2]) * S.inv_nu * z0;                   // P_r
+        rec[2] = rec[3] = 0.0;
+        rec[4] = S.term1 * B0 * wr;
+    } else if constexpr (COP == CVQ_GAUSSIAN) {
+        rec[0] = S.Ri[0] * (z0 * z0);
+        rec[1] = (S.Ri[1] + S.Ri[2]) * z0;
+        rec[2] = rec[3] = 0.0;
+        rec[4] = S.term1 * B0 * wr;
+    } else {
+        const double th = S.theta, a1 = th - 1.0, u = z0;
+        rec[0] = th * fma(a1, u, 1.0);                                   // num = c0 + c1 v
+        rec[1] = th * a1 * fma(-2.0, u, 1.0);
+        rec[2] = fma(a1, u, 1.0);                                        // d1 = c2 + a1 v
+        rec[3] = fma(a1, 1.0 - u, 1.0);                                  // d2 = c3 - a1 v
+        rec[4] = B0 * wr;
+    }
+}
+
+template <int COP>
+__device__ __forceinline__ FastRow load_fast_row(const double* rec) {
+    FastRow f;
+    const double2 a = *(const double2*)rec;
+    f.c0 = a.x;
+    f.c1 = a.y;
+    if constexpr (COP == CVQ_PLACKETT) {
+        const double2 b = *(const double2*)(rec + 2);
+        f.c2 = b.x;
+        f.c3 = b.y;
+    } else {
+        f.c2 = f.c3 = 0.0;
+    }
+    f.scale = rec[4];
+    return f;
+}
+
+template <int COP, int PM>
+__device__ __forceinline__ double fast_f(const StaticDev& S, const FastRow& f, double zc) {
+    if constexpr (COP == CVQ_STUDENT) {
+        const double b = fma(zc, fma(zc, S.Ri[3] * S.inv_nu, f.c1), f.c0);
+        if constexpr (PM == 8) {                      // nu = 6: b^-4; 1/inf = 0, 1/NaN = NaN
+            double y = __builtin_amdgcn_rcp(b);
+            y = fma(y, fma(-b, y, 1.0), y);
+            const double y2 = y * y;
+            return y2 * y2;
+        } else {
+            return pow_node_t<PM>(b, S.node_m, S.node_ex);
+        }
+    } else if constexpr (COP == CVQ_GAUSSIAN) {
+        const double qf = fma(zc, fma(zc, S.Ri[3], f.c1), f.c0);
+        return exp(-0.5 * qf);
+    } else {
+        const double a1 = S.theta - 1.0;
+        const double num = fma(f.c1, zc, f.c0);
+        const double d = fma(a1, zc, f.c2) * fma(-a1, zc, f.c3);
+        const double den = d * d;
+        double y = __builtin_amdgcn_rcp(den);
+        y = fma(y, fma(-den, y, 1.0), y);
+        y = fma(y, fma(-den, y, 1.0), y);
+        // num / 0 as IEEE division gives it (the Newton steps would give NaN)
+        return den == 0.0 ? (num == 0.0 ? __builtin_nan("") : __builtin_copysign(__builtin_inf(), num)) : num * y;
+    }
+}
+
+// Generic node: reference semantics (node_value); cg = (B_j, wc_j); W = wr * wc
+// (rank 1) or the full sum_ab pi[a][b] F0_a(r) F1_b(j).
+template <int COP, bool MSM>
+__device__ __forceinline__ double generic_node(const StaticDev& S, const double* rrec, double zc, const double* cg, int r,
+                                               int j, bool rank1, const double* pit) {
+    const RowCtx ctx = make_row<COP, 2>(S, rrec[5], 0.0, rrec[6]);
+    double W;
+    if (rank1) {
+        W = rrec[7] * cg[1];
+    } else {
+        const int q = S.q, n = S.n;
+        W = 0.0;
+        for (int b = 0; b < q; ++b) {
+            double g = 0.0;
+            for (int a2 = 0; a2 < q; ++a2) g = fma(pit[a2 * q + b], S.F[(size_t)a2 * n + r], g);
+            W = fma(g, S.F[((size_t)q + b) * n + j], W);
+        }
+    }
+    return node_value<COP, MSM, 2>(S, ctx, zc, cg[0], W);
+}
+
+// table_entry of grid index i on axis 0 (row) and axis 1 (column) at once: the
+// same arithmetic, with the Student quantile free of data-dependent branches so
+// the two entries' table gathers are in flight together.
+template <int COP, bool MSM, bool FUSED>
+__device__ __forceinline__ void table_pair(const StaticDev& S, const double* __restrict__ a,
+                                           const double* __restrict__ tA, const double* __restrict__ tB, long long t,
+                                           int i, double* A, double* B) {
+    if constexpr (!FUSED) {
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) {
+            A[ax] = tA[(t * 2 + ax) * S.n + i];
+            B[ax] = tB[(t * 2 + ax) * S.n + i];
+        }
+    } else if constexpr (COP == CVQ_STUDENT) {
+        double u[2], pdf[2];
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) marginal_u<MSM>(S, a, t * 2 + ax, ax, i, &u[ax], &pdf[ax]);
+        double z[2];
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) z[ax] = stdtrit_tab_bf(S.tk, u[ax]);      // student.py:102
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) {
+            const double uni = isfinite(z[ax])
+                ? S.g_uni * pow_half_neg(1.0 + (z[ax] * z[ax]) / S.nu, S.uni_m, S.uni_ex) : 0.0;   // :164-172
+            A[ax] = z[ax];
+            B[ax] = (1.0 / uni) * pdf[ax];
+        }
+    } else {
+#pragma unroll
+        for (int ax = 0; ax < 2; ++ax) table_entry<COP, MSM>(S, a, t * 2 + ax, ax, i, &A[ax], &B[ax]);
+    }
+}
+
+template <int NT>
+constexpr int kWtotInts = ((NT / 64) + 3) & ~3;
+
+// ------------------------------------------------------------------ the kernel
+// calc_var solve: snapshots + header, fused finalize when P.fin_var.
+// Thread tid owns rows tid + NT k (k < RPT, RPT = ceil(n / NT)); NT = 64 makes the
+// whole solve one wavefront: no barriers, no LDS round trips in the reductions.
+// FUSED: evaluate the date's tables here; else read k_tables' tA / tB.
+template <int COP, bool MSM, int NT, int RPT, int PM, bool FUSED>
+__global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, CompactGeom G, const double* __restrict__ a,
+                                                const double* __restrict__ tA, const double* __restrict__ tB,
+                                                const double* __restrict__ pi, double* __restrict__ stamps_out,
+                                                double* __restrict__ snaps, Header* hdr) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int n = S.n, tid = threadIdx.x, lane = tid & 63;
+    const long long t = blockIdx.x;
+    double* col = lds;                              // [n][kColRec]: z_j, B'_j = B_j wc_j
+    double* colg = col + kColRec * n;               // [n][2]: B_j, wc_j (generic path)
+    double* rowr = colg + 2 * n;                    // [n][kRowRec]: c0 c1 c2 c3 scale | z0 B0 wr
+    double* sx = rowr + kRowRec * n;                // [n] grid
+    double2* tail = (double2*)(sx + n);             // [kTailCap] tail nodes: (v*, value)
+    double* red = (double*)(tail + kTailCap);       // [2][3][NT / 64] reduction slots
+    int* wtot = (int*)(red + 6 * (NT / 64));        // [NT / 64] scan slots (padded to 16 B)
+    int16_t* cfx = (int16_t*)(wtot + kWtotInts<NT>);   // [n][kCutFixed] fixed-level cuts (16-B aligned)
+    int16_t* bk = cfx + (size_t)kCutFixed * n;      // [nb] grid lookup buckets
+    __shared__ int flags;                           // bit 0: non-finite table entry, bit 1: pi not rank 1
+
+    unsigned long long* stamps = stamps_out ? (unsigned long long*)stamps_out + t * 32 : nullptr;
+    auto stamp = [&](int idx) {                     // diagnostic only (never in a timed run)
+        if (stamps && tid == 0 && idx < 32) stamps[idx] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
+    if (stamps && tid == 0) stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+    int row[RPT];
+    bool own[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        row[k] = tid + NT * k;
+        own[k] = row[k] < n;
+    }
+    for (int w = tid; w < kCutFixed * n / 8; w += NT) ((int4*)cfx)[w] = ((const int4*)G.cutfix)[w];
+    for (int b = tid; b < G.nb; b += NT) bk[b] = G.bucket[b];
+    for (int i = tid; i < n; i += NT) sx[i] = S.x[i];
+    if (tid == 0) flags = 0;
+    __syncthreads();
+
+    // ---- tables: index i -> row record i (axis 0) and column record i (axis 1)
+    const int q = MSM ? S.q : 1;
+    const double* fb = MSM ? a + t * 2 * q : nullptr;          // forecasts_by_states[t] (2, q)
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        if (!own[k]) continue;
+        const int i = row[k];
+        double A[2], B[2];
+#ifdef CVQ_ABL_TABLES
+        A[0] = A[1] = sx[i] * 0.5;
+        B[0] = B[1] = 1.0;
+#else
+        table_pair<COP, MSM, FUSED>(S, a, tA, tB, t, i, A, B);
+#endif
+        double wr, wc;                                             // row / column weight factors
+        if constexpr (MSM) {
+            wr = wc = 0.0;
+            for (int b = 0; b < q; ++b) {
+                wr = fma(fb[b], S.F[(size_t)b * n + i], wr);
+                wc = fma(fb[q + b], S.F[((size_t)q + b) * n + i], wc);
+            }
+        } else {
+            wr = S.F[i];
+            wc = S.F[(size_t)n + i];
+        }
+        if (!isfinite(A[0]) || !isfinite(B[0]) || !isfinite(A[1]) || !isfinite(B[1])) bad |= 1;
+        col[kColRec * i] = A[1];
+        col[kColRec * i + 1] = B[1] * wc;
+        colg[2 * i] = B[1];
+        colg[2 * i + 1] = wc;
+        double* rr = rowr + kRowRec * i;
+        fast_row_consts<COP>(S, A[0], B[0], wr, rr);
+        rr[5] = A[0];
+        rr[6] = B[0];
+        rr[7] = wr;
+    }
+    const double* pit = pi + t * S.Q;
+    if constexpr (MSM) {                                          // rank-1 check of pi_t
+        for (int l = tid; l < S.Q; l += NT)
+            if (!(pit[l] == fb[l / q] * fb[q + l % q])) bad |= 2;
+    }
+    if (bad) atomicOr(&flags, bad);
+    __syncthreads();
+    stamp(1);
+    const int fl = flags;
+    const bool rank1 = !(fl & 2);
+    const bool fast = rank1 && (MSM || !(fl & 1));
+    double lev[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) lev[k] = sx[own[k] ? row[k] : 0] * S.w1;   // integration_algo.py:20 (2-D)
+    int parity = 0;
+
+    // sum of row rr's nodes j in [j0, j1] (fast path: row scale included, kIlp
+    // independent chains; generic: node values)
+    auto range_sum = [&](int rr, int j0, int j1) -> double {
+#ifndef CVQ_COMPACT_NOGENERIC
+        if (!fast) {
+            double acc = 0.0;
+            for (int j = j0; j <= j1; ++j)
+                acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + 2 * j, rr, j, rank1,
+                                              pit);
+            return acc;
+        }
+#endif
+        const FastRow fr = load_fast_row<COP>(rowr + kRowRec * rr);
+        constexpr int IL = (COP == CVQ_STUDENT && PM == 0) ? 1 : kIlp;   // general pow: register bound
+        double acc[IL];
+#pragma unroll
+        for (int u = 0; u < IL; ++u) acc[u] = 0.0;
+        int j = j0;
+        for (; j + IL - 1 <= j1; j += IL) {
+#pragma unroll
+            for (int u = 0; u < IL; ++u) {
+                const double2 cz = *(const double2*)(col + kColRec * (j + u));
+                acc[u] = fma(fast_f<COP, PM>(S, fr, cz.x), cz.y, acc[u]);
+            }
+        }
+        for (; j <= j1; ++j) {
+            const double2 cz = *(const double2*)(col + kColRec * j);
+            acc[0] = fma(fast_f<COP, PM>(S, fr, cz.x), cz.y, acc[0]);
+        }
+#pragma unroll
+        for (int h = 1; h < IL; h <<= 1)
+#pragma unroll
+            for (int u = 0; u + h < IL; u += 2 * h) acc[u] += acc[u + h];
+        return fr.scale * acc[0];
+    };
+    // one level's workgroup sums: slab (ka, kb] sum, its node count, bracket (blo, bhi] nodes
+    double sums[3];
+    auto level_sums = [&](const int (&ka)[RPT], const int (&kb)[RPT], const int (&blo)[RPT], const int (&bhi)[RPT]) {
+        double part = 0.0;
+        int ns = 0, nb = 0;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int len = own[k] ? max(kb[k] - ka[k], 0) : 0;
+            if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
+            ns += len;
+            nb += own[k] ? max(bhi[k] - blo[k], 0) : 0;
+        }
+        team_sum3<NT>(part, (double)ns, (double)nb, red, parity, sums);
+    };
+    auto fixcut = [&](int k, double v) {                         // one of the solve's fixed levels
+        const int16_t* c = cfx + (size_t)(own[k] ? row[k] : 0) * kCutFixed;
+        return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
+             : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : v == P.vmax ? c[kCutVmax]
+             : grid_count(sx, bk, G, (v - lev[k]) / S.w0, 0, n - 1);
+    };
+    int zero[RPT], ka[RPT], kb[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) zero[k] = 0;
+
+    // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) { ka[k] = fixcut(k, P.lower); kb[k] = fixcut(k, P.fg); }
+    level_sums(ka, kb, zero, zero);
+    const double r0 = sums[0];
+    stamp(2);
+    const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+    const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+    const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) { ka[k] = fixcut(k, nl); kb[k] = fixcut(k, nu); }
+    level_sums(ka, kb, zero, zero);
+    const double nr = sums[0];
+    const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
+    stamp(3);
+    double lo = __builtin_nan(""), hi = __builtin_nan("");
+    if (F > P.obj) { lo = P.vmin; hi = P.sg0; }
+    if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; }
+    if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; }
+    if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; }
+    bool ustack = !(hi == P.sg0 || hi == P.sg1);
+    int kLo[RPT], kHi[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {                              // NaN bracket (Q3): empty
+        kLo[k] = (own[k] && lo == lo) ? fixcut(k, lo) : 0;
+        kHi[k] = (own[k] && lo == lo) ? max((int)fixcut(k, hi), kLo[k]) : 0;
+    }
+    stamp(4);
+
+    // ---- (iv) bisection (:250-309); Q2 / Q4 are resolved across dates by the finalize
+    double prev = F, prevU = prevU0;
+    int nt = -1, it = 0;
+    uint64_t mask = 0;
+    double* sn = snaps + t * P.stride;
+    // the tail runs on wave 0; its lane 0 owns the header (rotating the tail wave
+    // by date, to spread the tails of a CU's dates over its SIMDs, measured slower)
+    const int leader = 0;
+    int nbr_next = 1 << 30;                                      // bracket nodes after the level
+    for (; it < P.K && nbr_next > kTailCap; ++it) {
+        const double mid = (lo + hi) / 2;
+        if (tid == 0) sn[it] = mid;
+        if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+        int kM[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+#ifdef CVQ_ABL_CNT
+            kM[k] = own[k] ? (kLo[k] + kHi[k]) >> 1 : 0;
+#else
+            kM[k] = own[k] ? grid_count(sx, bk, G, (mid - lev[k]) / S.w0, kLo[k], kHi[k]) : 0;   // Q10
+#endif
+            ka[k] = ustack ? kLo[k] : kM[k];
+            kb[k] = ustack ? kM[k] : kHi[k];
+        }
+        level_sums(ka, kb, kLo, kHi);
+        const double val = sums[0];
+        const int Ns = (int)sums[1], Nbr = (int)sums[2];
+        const int Nlow = ustack ? Ns : Nbr - Ns;                 // nodes of (lo, mid]
+        const double slab_lower = ustack ? lo : mid;
+        const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
+        if (Fn != 0.0) mask |= (1ull << it);
+        ustack = Fn < P.obj;
+        if (ustack) {
+            lo = mid;
+            nbr_next = Nbr - Nlow;
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) kLo[k] = kM[k];
+        } else {
+            hi = mid;
+            nbr_next = Nlow;
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) kHi[k] = kM[k];
+        }
+        prev = Fn;
+        prevU = mid;
+        if (it < 15) stamp(5 + it);
+    }
+
+    // ---- tail: the bracket's nodes -> LDS, wave 0 finishes the levels
+    if (it < P.K) {
+        int len = 0;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) len += own[k] ? kHi[k] - kLo[k] : 0;
+        int total;
+        int off = block_excl_scan<NT>(len, wtot, &total);
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            if (!own[k]) continue;
+            for (int j = kLo[k] + 1; j <= kHi[k] && off < kTailCap; ++j, ++off)   // total <= kTailCap
+                tail[off] = make_double2(G.vstar[(size_t)row[k] * n + j], range_sum(row[k], j, j));
+        }
+        __syncthreads();
+        stamp(29);
+#ifdef CVQ_ABL_TAIL
+        if (false) {
+#else
+        if ((tid >> 6) == (leader >> 6)) {
+#endif
+            // this lane's entries lane + 64 m: (v*, value); padding v* = NaN is in no interval
+            const int tot = min(total, kTailCap);
+            double tx[kTailPerLane], ty[kTailPerLane];
+#pragma unroll
+            for (int m = 0; m < kTailPerLane; ++m) {
+                const bool ok = lane + 64 * m < tot;
+                const double2 e = ok ? tail[lane + 64 * m] : make_double2(__builtin_nan(""), 0.0);
+                tx[m] = e.x;
+                ty[m] = e.y;
+            }
+            for (; it < P.K; ++it) {
+                const double mid = (lo + hi) / 2;
+                if (tid == leader) sn[it] = mid;
+                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+                const double a0 = ustack ? lo : mid, b0 = ustack ? mid : hi;   // slab (a0, b0]
+                double p = 0.0;
+#pragma unroll
+                for (int m = 0; m < kTailPerLane; ++m) p += (tx[m] > a0 && tx[m] <= b0) ? ty[m] : 0.0;
+                const double val = wave_sum(p);
+                const double slab_lower = ustack ? lo : mid;
+                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
+                if (Fn != 0.0) mask |= (1ull << it);
+                ustack = Fn < P.obj;
+                if (ustack) lo = mid; else hi = mid;
+                prev = Fn;
+                prevU = mid;
+            }
+        }
+    }
+    stamp(31);
+    if (stamps && tid == 0) stamps[26] = __builtin_amdgcn_s_memrealtime();
+
+    __shared__ int last;
+    if (tid == leader) {
+        sn[P.K] = (lo + hi) / 2;
+        if (nt < 0 && !(hi - lo > P.tol)) nt = P.K;
+        if (nt < 0) atomicOr(&hdr->error, 1);
+        else atomicMax(&hdr->iters, nt);
+        atomicOr((unsigned long long*)&hdr->nonzero, (unsigned long long)mask);
+        if (P.fin_var) {
+            __threadfence();                             // release: this date's snapshots + header bits
+            last = atomicAdd(&P.fin_err[3], 1) == (int)gridDim.x - 1;
+        }
+    }
+    if (!P.fin_var) return;
+    __syncthreads();
+    if (!last) return;
+    // k_finalize for a single rank, run by the last workgroup (calc_var_class.py:278, :293, :171)
+    __threadfence();                                     // acquire: every workgroup's stores
+    const int Nit = __hip_atomic_load(&hdr->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int err = __hip_atomic_load(&hdr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (Nit > P.K ? 2 : 0);
+    const unsigned long long nz = __hip_atomic_load((unsigned long long*)&hdr->nonzero, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    int kstop = min(Nit, P.K);
+    for (int k = 0; k < kstop; ++k)
+        if (!((nz >> k) & 1ull)) { kstop = k; break; }
+    for (long long d = tid; d < (long long)gridDim.x; d += NT)
+        P.fin_var[d] = snaps[d * P.stride + kstop] + P.ptf_mean;
+    __syncthreads();                                     // every thread has read the header
+    if (tid == 0) {
+        P.fin_err[0] = err;
+        P.fin_err[1] = kstop;
+        P.fin_err[2] = Nit;
+        P.fin_err[3] = 0;                                // ticket reset for the next launch
+        hdr->iters = 0;                                  // header reset for the next launch
+        hdr->error = 0;
+        hdr->nonzero = 0;
+    }
+}
+
+// LDS bytes of one k_compact workgroup
+inline size_t compact_lds_bytes(int n, int nt, int nb) {
+    return sizeof(double) * ((size_t)(kColRec + 2 + kRowRec + 1) * n) + sizeof(double2) * kTailCap +
+           sizeof(double) * 6 * (nt / 64) + sizeof(int) * (((nt / 64) + 3) & ~3) +
+           sizeof(int16_t) * ((size_t)kCutFixed * n + nb);
+}
+
+}  // namespace cvq

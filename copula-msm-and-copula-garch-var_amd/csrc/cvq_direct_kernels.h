@@ -64,8 +64,14 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
                                                         Header* hdr) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int NT = 256;
-    const int n = S.n, tid = threadIdx.x, slot = tid;
     const long long t = blockIdx.x;
+#if CVQ_DIRECT_ROT
+    // wave w owns row block (w + t) mod 4: the long rows of triangular slabs land on a
+    // different SIMD for each of the dates sharing a CU
+    const int n = S.n, tid = threadIdx.x, slot = ((((tid >> 6) + (int)t) & 3) << 6) | (tid & 63);
+#else
+    const int n = S.n, tid = threadIdx.x, slot = tid;
+#endif
     // Column records, one per inner index j, CS doubles each (16-B aligned):
     //   [0] z_j, [1..QT] F'_b[j], then B_j for the non-folded paths.
     // A lane's operands for a node are CS contiguous doubles (ds_read_b128 x CS/2);

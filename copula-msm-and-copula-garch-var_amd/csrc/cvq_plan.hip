@@ -14,7 +14,7 @@
 #include "cvq_common.h"
 #include "cvq_quad_kernels.h"
 #include "cvq_direct_kernels.h"
-#include "cvq_binned_kernels.h"
+#include "cvq_compact_kernels.h"
 #include "cvq_tppf_tables.h"
 
 namespace cvq {
@@ -144,11 +144,16 @@ struct cvq_plan {
     long long capIO = 0;
     double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
     unsigned long long* d_stamps = nullptr;   // diagnostic phase stamps (CVQ_STAMPS=1)
-    // BINNED: host grid copy + date-independent cut tables for the cached solve arguments
+    // COMPACT: host grid copy, v* table, grid lookup buckets, fixed-level cuts for the
+    // cached solve arguments
     std::vector<double> hx;
-    int16_t* d_cut = nullptr;    // cut1 [n][kE1+1] then cutB [3][n][kBins+1]
-    double bin_key[6] = {0, 0, 0, 0, 0, 0};
-    bool bin_valid = false;
+    double* d_vstar = nullptr;   // [n][n]
+    int16_t* d_bucket = nullptr; // [nb]
+    double bx0 = 0.0, binv = 0.0;
+    int nb = 0;
+    int16_t* d_cutfix = nullptr; // [n][kCutFixed]
+    double cut_key[6] = {0, 0, 0, 0, 0, 0};
+    bool cut_valid = false;
     long long capStamps = 0;
     // optional per-kernel timing (HIP events on the plan's stream)
     int timing = 0;              // bitmask of kernel kinds timed with HIP events
@@ -320,10 +325,11 @@ int ensure_stamps(cvq_plan* p) {
     return CVQ_OK;
 }
 
-// ---------------------------------------------------------------- BINNED
+// ---------------------------------------------------------------- COMPACT
 // Cut columns cnt_r(v) = largest j with x_j <= (v - x_r w1) / w0 (else 0), exactly
 // as the device's count_le over [0, n-1] (create_grids.py:104-108, Q9/Q10).
 int host_cnt(const std::vector<double>& x, double lev, double w0, double v) {
+    if (!(v == v)) return 0;                                   // NaN level: count_le keeps klo
     const double g = (v - lev) / w0;
     int lo = 0, hi = (int)x.size() - 1;
     while (lo < hi) {
@@ -333,73 +339,97 @@ int host_cnt(const std::vector<double>& x, double lev, double w0, double v) {
     return lo;
 }
 
-// Edges of the depth-kBinLevels bisection tree of (lo, hi]: the midpoints
-// (lo + hi) / 2 the reference computes at every node (calc_var_class.py:279).
-void tree_edges(double lo, double hi, double* ed) {
-    ed[0] = lo;
-    ed[kBins] = hi;
-    for (int s = kBins / 2; s >= 1; s >>= 1)
-        for (int e = s; e < kBins; e += 2 * s) ed[e] = (ed[e - s] + ed[e + s]) / 2;
+// Ordered-integer view of doubles (monotone for all non-NaN values).
+inline int64_t d2o(double d) {
+    int64_t b;
+    std::memcpy(&b, &d, 8);
+    return b >= 0 ? b : ~(b & INT64_MAX);
+}
+inline double o2d(int64_t o) {
+    const int64_t b = o >= 0 ? o : (~o) | INT64_MIN;
+    double d;
+    std::memcpy(&d, &b, 8);
+    return d;
 }
 
-// 0: cut tables ready for these arguments; 1: arguments outside the binned
-// layout (lower < sg0 < fg < sg1 < vmax, vmin < sg0 required); <0: error.
-int ensure_bingeom(cvq_plan* p, const SolveConst& P) {
-    const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
-    if (!(P.lower < P.sg0 && P.sg0 < P.fg && P.fg < P.sg1 && P.sg1 < P.vmax && P.vmin < P.sg0)) return 1;
-    if (p->bin_valid && std::memcmp(key, p->bin_key, sizeof key) == 0) return 0;
-    const int n = p->S.n;
-    const size_t n1 = (size_t)n * (kE1 + 1), nb = (size_t)3 * n * (kBins + 1);
-    std::vector<int16_t> h(n1 + nb);
-    double ed[kBins + 1];
-    tree_edges(P.sg1, P.vmax, ed);
+// v*(r, j): the smallest double v with x_j <= (v - lev_r) / w0, the exact FP64
+// membership rule of the nested grid (Q10): node (r, j >= 1) lies in the slab
+// (a, b] iff a < v* <= b, because (v - lev) / w0 is non-decreasing in v.
+void build_vstar(const std::vector<double>& x, double w0, double w1, std::vector<double>& out) {
+    const int n = (int)x.size();
+    out.assign((size_t)n * n, 0.0);
     for (int r = 0; r < n; ++r) {
-        const double lev = p->hx[r] * p->S.w1;                 // integration_algo.py:20 (2-D)
-        int16_t* c = h.data() + (size_t)r * (kE1 + 1);
-        c[0] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.lower);
-        c[1] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.sg0);
-        c[2] = (int16_t)host_cnt(p->hx, lev, p->S.w0, P.fg);
-        for (int e = 0; e <= kBins; ++e) c[3 + e] = (int16_t)host_cnt(p->hx, lev, p->S.w0, ed[e]);
-    }
-    const double br[3][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.fg, P.sg1}};
-    for (int b = 0; b < 3; ++b) {
-        tree_edges(br[b][0], br[b][1], ed);
-        for (int r = 0; r < n; ++r) {
-            const double lev = p->hx[r] * p->S.w1;
-            int16_t* c = h.data() + n1 + ((size_t)b * n + r) * (kBins + 1);
-            for (int e = 0; e <= kBins; ++e) c[e] = (int16_t)host_cnt(p->hx, lev, p->S.w0, ed[e]);
+        const double lev = x[r] * w1;                          // integration_algo.py:20 (2-D)
+        for (int j = 0; j < n; ++j) {
+            auto pred = [&](double v) { return x[j] <= (v - lev) / w0; };
+            const double g = x[j] * w0 + lev, h = 1e-9 * (std::fabs(g) + 1.0);
+            int64_t lo = d2o(g - h), hi = d2o(g + h);          // pred(lo) false, pred(hi) true
+            if (pred(o2d(lo)) || !pred(o2d(hi))) { lo = d2o(-HUGE_VAL); hi = d2o(HUGE_VAL); }
+            while (hi - lo > 1) {
+                const int64_t m = lo + (hi - lo) / 2;
+                if (pred(o2d(m))) hi = m; else lo = m;
+            }
+            out[(size_t)r * n + j] = o2d(hi);
         }
     }
-    p->bin_valid = false;
-    if (!p->d_cut) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cut, h.size() * sizeof(int16_t)));
-    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cut, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
+}
+
+// Grid lookup buckets: bucket b covers [x_0 + b h, x_0 + (b + 1) h); its entry is
+// the largest j with x_j <= x_0 + b h (0 if none), a start for grid_count's probe.
+void build_buckets(const std::vector<double>& x, std::vector<int16_t>& bk, double* bx0, double* binv) {
+    const int n = (int)x.size(), nb = kBucketsPerPoint * n;
+    const double h = (x[n - 1] - x[0]) / nb;
+    *bx0 = x[0];
+    *binv = h > 0.0 ? 1.0 / h : 0.0;
+    bk.assign(nb, 0);
+    int j = 0;
+    for (int b = 0; b < nb; ++b) {
+        const double edge = x[0] + b * h;
+        while (j + 1 < n && x[j + 1] <= edge) ++j;
+        bk[b] = (int16_t)j;
+    }
+}
+
+// Fixed-level cut table for the cached solve arguments.
+int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
+    const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
+    if (p->cut_valid && std::memcmp(key, p->cut_key, sizeof key) == 0) return CVQ_OK;
+    const int n = p->S.n;
+    std::vector<int16_t> h((size_t)n * kCutFixed, 0);
+    for (int r = 0; r < n; ++r) {
+        const double lev = p->hx[r] * p->S.w1;
+        for (int e = 0; e < 6; ++e) h[(size_t)r * kCutFixed + e] = (int16_t)host_cnt(p->hx, lev, p->S.w0, key[e]);
+    }
+    p->cut_valid = false;
+    if (!p->d_cutfix) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cutfix, h.size() * sizeof(int16_t)));
+    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cutfix, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
-    std::memcpy(p->bin_key, key, sizeof key);
-    p->bin_valid = true;
-    return 0;
+    std::memcpy(p->cut_key, key, sizeof key);
+    p->cut_valid = true;
+    return CVQ_OK;
 }
 
 }  // namespace
 namespace cvq {
-int launch_binned(const StaticDev& S, const SolveConst& P, const BinGeom& BG, long long T, hipStream_t stream,
-                  const double* a, const double* pi, double* st, double* snaps, Header* hdr);   // cvq_binned.hip
+int compact_max_n();                                                                  // cvq_compact.hip
+int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
+                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
+                   double* snaps, Header* hdr);
 }
 namespace {
 
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
-    if (p->strategy == CVQ_STRATEGY_BINNED && direct_fused(p)) {
-        int rc = ensure_bingeom(p, P);
-        if (rc < 0) return rc;
-        if (rc == 0) {
-            static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
-            double* st = nullptr;
-            if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
-            if (dbg_stamps) st = (double*)p->d_stamps;
-            const BinGeom BG{p->d_cut, p->d_cut + (size_t)p->S.n * (kE1 + 1)};
-            return launch_binned(p->S, P, BG, p->T, p->stream, p->in_a, p->in_pi, st, snaps, hdr);
-        }
-        // rc > 0: solve arguments outside the binned layout -> slab-by-slab k_direct
+    if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
+        int rc = ensure_cutfix(p, P);
+        if (rc) return rc;
+        static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
+        double* st = nullptr;
+        if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
+        if (dbg_stamps) st = (double*)p->d_stamps;
+        const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb};
+        return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
+                              snaps, hdr);
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
         // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
@@ -427,7 +457,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     TimedScope ts(p, TK_SLAB);
-    if (p->strategy != CVQ_STRATEGY_PREFIX) {      // BINNED: slabs of arbitrary bounds run k_direct
+    if (p->strategy != CVQ_STRATEGY_PREFIX) {      // COMPACT: slabs of arbitrary bounds run k_direct
         SolveConst P{};
         return launch_direct(p, P, 1, bounds, out, nullptr, nullptr);
     }
@@ -507,7 +537,7 @@ int dispatch_cop(cvq_plan* p, bool tables) {
 int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
-    if (p->strategy != CVQ_STRATEGY_PREFIX && direct_fused(p)) {   // k_direct / k_binned evaluate their tables
+    if (p->strategy != CVQ_STRATEGY_PREFIX && direct_fused(p)) {   // k_direct / k_compact evaluate their tables
         if (hdr) CVQ_HIP_CHECK(hipMemsetAsync(hdr, 0, sizeof(Header), p->stream));
         return CVQ_OK;
     }
@@ -629,9 +659,9 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
     CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
     CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX || s->strategy == CVQ_STRATEGY_DIRECT ||
-                    s->strategy == CVQ_STRATEGY_BINNED, CVQ_ERR_INVALID, "unknown strategy");
+                    s->strategy == CVQ_STRATEGY_COMPACT, CVQ_ERR_INVALID, "unknown strategy");
     CVQ_REQUIRE(!(s->strategy != CVQ_STRATEGY_PREFIX && s->dim != 2), CVQ_ERR_UNSUPPORTED,
-                "the DIRECT and BINNED strategies are built for dim == 2");
+                "the DIRECT and COMPACT strategies are built for dim == 2");
     for (int l = 0; l < Q; ++l) {             // create_vol_combinations ij order (msm_estimation.py:384)
         int rem = l;
         for (int d = s->dim - 1; d >= 0; --d) {
@@ -760,6 +790,20 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
         S.phi = p->d_phi;
     }
+    if (p->strategy == CVQ_STRATEGY_COMPACT) {         // exact level thresholds + grid lookup buckets
+        std::vector<double> vs;
+        build_vstar(p->hx, S.w0, S.w1, vs);
+        std::vector<int16_t> bk;
+        build_buckets(p->hx, bk, &p->bx0, &p->binv);
+        p->nb = (int)bk.size();
+        if ((rc = dev_alloc(&p->d_vstar, vs.size())) || (rc = dev_alloc(&p->d_bucket, bk.size()))) {
+            cvq_plan_destroy(p);
+            return rc;
+        }
+        e = hipMemcpy(p->d_vstar, vs.data(), vs.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_bucket, bk.data(), bk.size() * sizeof(int16_t), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+    }
     *out = p;
     return CVQ_OK;
 }
@@ -772,7 +816,8 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (auto& e : p->events) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
-                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps, (void*)p->d_cut})
+                    (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
+                    (void*)p->d_cutfix, (void*)p->d_vstar, (void*)p->d_bucket})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
@@ -930,7 +975,7 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;
-    // DIRECT / BINNED keep p->d_hdr zero themselves (zeroed at creation, reset by the fused finalize)
+    // DIRECT / COMPACT keep p->d_hdr zero themselves (zeroed at creation, reset by the fused finalize)
     if ((rc = ensure_mass(p, p->strategy != CVQ_STRATEGY_PREFIX ? nullptr : p->d_hdr))) return rc;
     bool exact;
     int K = bisect_budget(*a, &exact);

@@ -73,22 +73,30 @@ __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __res
 //   B   = pdf / univariate-copula-margin-pdf      (MSM: pdf = 1; Plackett: B = pdf)
 // Layout [T][dim][n], coalesced along i.
 // TAB: the plan has verified direct t.ppf tables (Student only; see stdtrit_tabulated).
-template <int COP, bool MSM, bool TAB = false>
-__device__ __forceinline__ void table_entry(const StaticDev& S, const double* __restrict__ a, long long td, int d,
-                                            int i, double* A_out, double* B_out) {
-    double u, pdf = 1.0;
+// Marginal CDF value u and density factor of grid index i on axis d, date row td.
+template <bool MSM>
+__device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __restrict__ a, long long td, int d, int i,
+                                           double* u_out, double* pdf_out) {
     if (MSM) {
         const double* f = a + td * S.q;
         const double* ph = S.phi + (size_t)d * S.q * S.n + i;
         double acc = f[0] * ph[0];
         for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
-        u = acc;                                                 // msm_integration_function.py:34-36
+        *u_out = acc;                                            // msm_integration_function.py:34-36
+        *pdf_out = 1.0;
     } else {
         const double sig = a[td];
         const double xs = S.x[i] / sig;                         // garch_integration_function.py:31
-        u = 0.5 * (1.0 + erf(xs / kInvSqrt2));                   // :33
-        pdf = (kInvSqrt2Pi * exp(-0.5 * (xs * xs))) / sig;       // :38
+        *u_out = 0.5 * (1.0 + erf(xs / kInvSqrt2));              // :33
+        *pdf_out = (kInvSqrt2Pi * exp(-0.5 * (xs * xs))) / sig;  // :38
     }
+}
+
+template <int COP, bool MSM, bool TAB = false>
+__device__ __forceinline__ void table_entry(const StaticDev& S, const double* __restrict__ a, long long td, int d,
+                                            int i, double* A_out, double* B_out) {
+    double u, pdf;
+    marginal_u<MSM>(S, a, td, d, i, &u, &pdf);
     if (COP == CVQ_PLACKETT) {
         *A_out = u;
         *B_out = pdf;

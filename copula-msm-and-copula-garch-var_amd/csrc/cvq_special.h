@@ -262,6 +262,24 @@ __host__ __device__ __forceinline__ double stdtrit_tabulated(const TConst& k, do
     return upper ? -t : t;
 }
 
+// stdtrit_tabulated without data-dependent branches: the same arithmetic (both
+// table variables evaluated, one selected), so a thread can keep two
+// evaluations' table gathers in flight together.
+__device__ __forceinline__ double stdtrit_tab_bf(const TConst& k, double p) {
+    const bool upper = p > 0.5;
+    const double pp = upper ? (1.0 - p) : p;                   // exact
+    const bool centre = pp >= k.p_split;
+    const double d = 0.5 - pp;
+    const double v = exp(log(pp) * k.inv_nu);
+    const double q = centre ? quintic(k.q_c, k.n_qc, d * k.inv_qc) : quintic(k.q_v, k.n_qv, v * k.inv_qv);
+    double t = centre ? d * q : -1.0 / (v * q);
+    t = upper ? -t : t;
+    if (p == 0.5) t = 0.0;
+    if (p == 0.0) t = -pos_inf();
+    if (p == 1.0) t = pos_inf();
+    return (p >= 0.0 && p <= 1.0) ? t : __builtin_nan("");
+}
+
 // Student-t quantile t.ppf(p, nu) (scipy semantics: 0 -> -inf, 1 -> +inf, outside -> nan).
 __host__ __device__ inline double stdtrit(const TConst& k, double p) {
     if (!(p >= 0.0 && p <= 1.0) || !(k.nu > 0.0)) return __builtin_nan("");

@@ -47,7 +47,7 @@ extern "C" {
 /* quadrature strategy (both reproduce the reference) */
 #define CVQ_STRATEGY_PREFIX 0    /* materialise per-date row-prefix joint mass, then solve */
 #define CVQ_STRATEGY_DIRECT 1    /* evaluate each slab's nodes inside the solve kernel     */
-#define CVQ_STRATEGY_BINNED 2    /* one pass fills bisection-tree bins, 4 levels per block */
+#define CVQ_STRATEGY_COMPACT 2   /* DIRECT control flow, one barrier per level, one-wave tail */
 
 typedef struct cvq_plan cvq_plan;
 

@@ -32,7 +32,7 @@ def _plan(z, sl, strategy):
     return p
 
 
-@pytest.mark.parametrize("strategy", ["binned", "direct", "prefix"])
+@pytest.mark.parametrize("strategy", ["compact", "direct", "prefix"])
 @pytest.mark.parametrize("case,ranks", [("cfg1", 2), ("cfg1", 3), ("q1_lowvol", 4), ("cfg2_n64", 3),
                                         ("cfg3_n128", 2), ("cfg5_n64", 2)])
 def test_sharded_device_solve(case, ranks, strategy):

@@ -33,7 +33,7 @@ for k, d in sorted(summ.items()):
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {v:16.1f}")
-dom = "k_mass" if strategy == "prefix" else "k_direct"
+dom = {"prefix": "k_mass", "compact": "k_compact"}.get(strategy, "k_direct")
 mass = [k for k in summ if re.search(rf"\b{dom}\b", k)]
 if mass:
     d = summ[mass[0]]
