@@ -442,22 +442,39 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
              : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : v == P.vmax ? c[kCutVmax]
              : grid_count(sx, bk, G, (v - lev[k]) / S.w0, 0, n - 1);
     };
-    int zero[RPT], ka[RPT], kb[RPT];
+    int ka[RPT], kb[RPT];
+    // slab (va, vb] between two fixed levels: these are triangles and corner bands
+    // whose row lengths run from 0 to ~n, so the owner of row r sums the first half
+    // of row r and the second half of row n - 1 - r (long rows pair with short ones)
+    auto fixed_slab = [&](double va, double vb) {
+        double part = 0.0;
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) zero[k] = 0;
+        for (int k = 0; k < RPT; ++k) {
+            if (!own[k]) continue;
+            const int r1 = row[k], r2 = n - 1 - row[k];
+            const int16_t* c1 = cfx + (size_t)r1 * kCutFixed;
+            const int16_t* c2 = cfx + (size_t)r2 * kCutFixed;
+            auto cut = [&](const int16_t* c, double v) {
+                return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
+                     : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : c[kCutVmax];
+            };
+            const int a1 = cut(c1, va), b1 = max((int)cut(c1, vb), a1);
+            const int a2 = cut(c2, va), b2 = max((int)cut(c2, vb), a2);
+            const int m1 = a1 + (b1 - a1 + 1) / 2, m2 = a2 + (b2 - a2 + 1) / 2;
+            if (m1 > a1) part += range_sum(r1, a1 + 1, m1);
+            if (b2 > m2) part += range_sum(r2, m2 + 1, b2);
+        }
+        team_sum3<NT>(part, 0.0, 0.0, red, parity, sums);
+    };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) { ka[k] = fixcut(k, P.lower); kb[k] = fixcut(k, P.fg); }
-    level_sums(ka, kb, zero, zero);
+    fixed_slab(P.lower, P.fg);
     const double r0 = sums[0];
     stamp(2);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) { ka[k] = fixcut(k, nl); kb[k] = fixcut(k, nu); }
-    level_sums(ka, kb, zero, zero);
+    fixed_slab(nl, nu);
     const double nr = sums[0];
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);
@@ -599,8 +616,20 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     int kstop = min(Nit, P.K);
     for (int k = 0; k < kstop; ++k)
         if (!((nz >> k) & 1ull)) { kstop = k; break; }
-    for (long long d = tid; d < (long long)gridDim.x; d += NT)
-        P.fin_var[d] = snaps[d * P.stride + kstop] + P.ptf_mean;
+    // every load in flight before the first store: one memory latency for T <= 4 NT
+    for (long long d0 = tid; d0 < (long long)gridDim.x; d0 += 4 * NT) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            v[u] = d < (long long)gridDim.x ? snaps[d * P.stride + kstop] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            if (d < (long long)gridDim.x) P.fin_var[d] = v[u] + P.ptf_mean;
+        }
+    }
     __syncthreads();                                     // every thread has read the header
     if (tid == 0) {
         P.fin_err[0] = err;

@@ -340,8 +340,20 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     int kstop = min(N, P.K);
     for (int k = 0; k < kstop; ++k)
         if (!((nz >> k) & 1ull)) { kstop = k; break; }
-    for (long long d = tid; d < (long long)gridDim.x; d += NT)
-        P.fin_var[d] = snaps[d * P.stride + kstop] + P.ptf_mean;
+    // every load in flight before the first store: one memory latency for T <= 4 NT
+    for (long long d0 = tid; d0 < (long long)gridDim.x; d0 += 4 * NT) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            v[u] = d < (long long)gridDim.x ? snaps[d * P.stride + kstop] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            if (d < (long long)gridDim.x) P.fin_var[d] = v[u] + P.ptf_mean;
+        }
+    }
     __syncthreads();                                     // every thread has read the header
     if (tid == 0) {
         P.fin_err[0] = e;

@@ -42,6 +42,8 @@ tot = st[:, -1] - st[:, 0]
 print(f"per-WG total cycles: mean {tot.mean():.0f}  max {tot.max():.0f}")
 for i, nm in enumerate(names):
     print(f"  {nm:9s} mean {d[:, i].mean():9.0f}  max {d[:, i].max():9.0f}")
+slow = np.argsort(tot)[-max(1, T // 20):]        # slowest 5% of the workgroups
+print("slowest 5%: mean cycles by phase:", " ".join(f"{nm}={d[slow, i].mean():.0f}" for i, nm in enumerate(names)))
 if STRAT != "direct":
     r0 = rt[:, 0] - rt[:, 0].min()
     r1 = rt[:, 1] - rt[:, 0].min()
