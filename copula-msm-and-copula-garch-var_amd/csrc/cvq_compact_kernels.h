@@ -255,6 +255,9 @@ __device__ __forceinline__ double generic_node(const StaticDev& S, const double*
     return node_value<COP, MSM, 2>(S, ctx, zc, cg[0], W);
 }
 
+#ifndef CVQ_TABLE_BRANCHY
+#define CVQ_TABLE_BRANCHY 0
+#endif
 // table_entry of grid index i on axis 0 (row) and axis 1 (column) at once: the
 // same arithmetic, with the Student quantile free of data-dependent branches so
 // the two entries' table gathers are in flight together.
@@ -268,7 +271,7 @@ __device__ __forceinline__ void table_pair(const StaticDev& S, const double* __r
             A[ax] = tA[(t * 2 + ax) * S.n + i];
             B[ax] = tB[(t * 2 + ax) * S.n + i];
         }
-    } else if constexpr (COP == CVQ_STUDENT) {
+    } else if constexpr (COP == CVQ_STUDENT && !CVQ_TABLE_BRANCHY) {
         double u[2], pdf[2];
 #pragma unroll
         for (int ax = 0; ax < 2; ++ax) marginal_u<MSM>(S, a, t * 2 + ax, ax, i, &u[ax], &pdf[ax]);
@@ -284,7 +287,7 @@ __device__ __forceinline__ void table_pair(const StaticDev& S, const double* __r
         }
     } else {
 #pragma unroll
-        for (int ax = 0; ax < 2; ++ax) table_entry<COP, MSM>(S, a, t * 2 + ax, ax, i, &A[ax], &B[ax]);
+        for (int ax = 0; ax < 2; ++ax) table_entry<COP, MSM, COP == CVQ_STUDENT>(S, a, t * 2 + ax, ax, i, &A[ax], &B[ax]);
     }
 }
 
