@@ -225,6 +225,18 @@ def garch_loglik(returns, params, device: int = 0) -> np.ndarray:
     return out
 
 
+def garch_loglik_pq(returns, p: int, q: int, params, device: int = 0) -> np.ndarray:
+    """params (B, 1 + p + q) rows (omega, alpha_1..alpha_p, beta_1..beta_q) -> (B,) log-likelihoods
+    (numba_garch_log_likelihood, garch/estimation.py:91-125)."""
+    r, pp = N.f64(returns), N.f64(np.atleast_2d(params))
+    if pp.shape[1] != 1 + p + q:
+        raise ValueError(f"GARCH({p},{q}) parameter rows have {1 + p + q} entries, got {pp.shape[1]}")
+    out = np.empty(pp.shape[0])
+    N.check(N.lib().cvq_garch_loglik_pq(device, int(p), int(q), N.ptr(pp), pp.shape[0], N.ptr(r), r.size,
+                                        N.ptr(out), N.MEM_HOST), "cvq_garch_loglik_pq")
+    return out
+
+
 def ukf_loglik(returns, params, device: int = 0) -> np.ndarray:
     """params (B, 3) rows (a, l, q)."""
     r, p = N.f64(returns), N.f64(np.atleast_2d(params))

@@ -203,6 +203,59 @@ __global__ void k_garch_loglik(const double* __restrict__ prm, long long B, cons
     out[b] = -0.5 * acc;
 }
 
+// GARCH(p, q) log-likelihood of numba_garch_log_likelihood (garch/estimation.py:91-125)
+// for a batch of parameter rows [omega, alpha_1..alpha_p, beta_1..beta_q], one
+// thread per row: sigma2[0] = omega / (1 - sum(alpha) - sum(beta)); sigma2[t] =
+// max(omega + sum_{i < min(p,t)} alpha_i r[t-i-1]^2 + sum_{j < min(q,t)} beta_j
+// sigma2[t-j-1], 1e-7); LL = -0.5 sum_{t >= max(p,q)} log(2 pi sigma2_t) + r_t^2 / sigma2_t.
+// The last q variances live in a register ring (P, Q <= kGarchMaxPQ).
+constexpr int kGarchMaxPQ = 4;
+template <int P, int Q>
+__global__ void k_garch_loglik_pq(const double* __restrict__ prm, long long B, const double* __restrict__ r,
+                                  long long N, double* __restrict__ out) {
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double* pr = prm + b * (1 + P + Q);
+    const double omega = pr[0];
+    double alpha[P], beta[Q], sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) { alpha[i] = pr[1 + i]; sa += alpha[i]; }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) { beta[j] = pr[1 + P + j]; sb += beta[j]; }
+    double hist[Q];                                   // hist[j] = sigma2[t - 1 - j]
+#pragma unroll
+    for (int j = 0; j < Q; ++j) hist[j] = 0.0;
+    hist[0] = omega / (1 - sa - sb);                  // estimation.py:106 (np.sum order)
+    constexpr int M = P > Q ? P : Q;                  // extra_size: chopped prefix (:119-121)
+    double acc = 0.0;
+    for (long long t = 1; t < N; ++t) {
+        double v = omega;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (i < t) v += alpha[i] * (r[t - i - 1] * r[t - i - 1]);
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+            if (j < t) v += beta[j] * hist[j];
+        const double s2 = (v < 1e-7) ? 1e-7 : v;      // max(sigma2[t], epsilon)
+#pragma unroll
+        for (int j = Q - 1; j > 0; --j) hist[j] = hist[j - 1];
+        hist[0] = s2;
+        if (t >= M) acc += log(2 * M_PI * s2) + (r[t] * r[t]) / s2;
+    }
+    out[b] = -0.5 * acc;
+}
+
+template <int P>
+void launch_garch_pq(int q, const double* p, long long B, const double* r, long long N, double* o) {
+    const dim3 g((unsigned)((B + 63) / 64)), blk(64);
+    switch (q) {
+        case 1: hipLaunchKernelGGL((k_garch_loglik_pq<P, 1>), g, blk, 0, 0, p, B, r, N, o); break;
+        case 2: hipLaunchKernelGGL((k_garch_loglik_pq<P, 2>), g, blk, 0, 0, p, B, r, N, o); break;
+        case 3: hipLaunchKernelGGL((k_garch_loglik_pq<P, 3>), g, blk, 0, 0, p, B, r, N, o); break;
+        default: hipLaunchKernelGGL((k_garch_loglik_pq<P, 4>), g, blk, 0, 0, p, B, r, N, o); break;
+    }
+}
+
 // ----------------------------------------------------------------------- UKF
 struct UkfConst {
     double wm0, wm1, wc0, wc1, wm2_0, wm2_1, phi;
@@ -482,6 +535,29 @@ int32_t cvq_garch_loglik(int32_t device, const double* params, int64_t B, const 
         (rc = stage_out(out, B, mem, dout, &d_out)))
         return rc;
     hipLaunchKernelGGL(k_garch_loglik, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, 0, d_p, B, d_r, N, d_out);
+    return finish_out(out, B, mem, dout);
+}
+
+int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* params, int64_t B,
+                            const double* returns, int64_t N, double* out, int32_t mem) {
+    CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
+    CVQ_REQUIRE(p >= 1 && q >= 1 && p <= kGarchMaxPQ && q <= kGarchMaxPQ, CVQ_ERR_UNSUPPORTED,
+                "GARCH orders must be 1 <= p, q <= 4");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf pin, rin, dout;
+    const double *d_p, *d_r;
+    double* d_out;
+    if ((rc = stage_in(params, (size_t)B * (1 + p + q), mem, pin, &d_p)) || (rc = stage_in(returns, N, mem, rin, &d_r)) ||
+        (rc = stage_out(out, B, mem, dout, &d_out)))
+        return rc;
+    switch (p) {
+        case 1: launch_garch_pq<1>(q, d_p, B, d_r, N, d_out); break;
+        case 2: launch_garch_pq<2>(q, d_p, B, d_r, N, d_out); break;
+        case 3: launch_garch_pq<3>(q, d_p, B, d_r, N, d_out); break;
+        default: launch_garch_pq<4>(q, d_p, B, d_r, N, d_out); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
     return finish_out(out, B, mem, dout);
 }
 

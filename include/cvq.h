@@ -171,6 +171,11 @@ int32_t cvq_garch_loglik(int32_t device, const double* params, int64_t B,
                          const double* returns, int64_t N, double* out, int32_t mem);
 int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B,
                        const double* returns, int64_t N, double* out, int32_t mem);
+/* GARCH(p, q), 1 <= p, q <= 4, for the (p, q) search of GarchOptimizer.optimize
+ * (garch/opti.py:89-137): params [B][1 + p + q] = (omega, alpha_1..p, beta_1..q);
+ * garch/estimation.py:91-125 incl. the max(p, q) chopped prefix. */
+int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* params, int64_t B,
+                            const double* returns, int64_t N, double* out, int32_t mem);
 
 /* Special functions on the device (known-answer tests against scipy):
  * fn 0 = t.ppf(u, nu) (student.py:102), 1 = norm.ppf (gaussian.py:44),

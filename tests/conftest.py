@@ -17,7 +17,8 @@ for p in (REPO, PKG_DIR):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-GOLDEN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f != "kat_special.npz")
+GOLDEN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN)
+                      if f.endswith(".npz") and f != "kat_special.npz" and not f.startswith("optim_"))
 
 
 def pytest_configure(config):
