@@ -24,8 +24,13 @@ from . import _native as N
 def student(cdf, nu, corr_matrix):
     """copulas/student/student.py:49-174."""
     u = np.asarray(cdf, dtype=np.float64)
-    P, d = u.shape
-    z = N.special("tppf", u, nu=float(nu))
+    return student_from_quantiles(N.special("tppf", u, nu=float(nu)), nu, corr_matrix)
+
+
+def student_from_quantiles(z, nu, corr_matrix):
+    """student.py:66-79 after the t.ppf step: the multivariate t pdf of the
+    quantiles z (P, d) over the product of the univariate t pdfs."""
+    P, d = z.shape
     Ri, det = np.linalg.inv(corr_matrix), np.linalg.det(corr_matrix)
     term1 = math.gamma((nu + d) / 2) / (math.gamma(nu / 2) * ((nu * np.pi) ** (d / 2)) * np.sqrt(det))
     g = math.gamma((nu + 1) / 2) / (np.sqrt(nu * np.pi) * math.gamma(nu / 2))
@@ -41,8 +46,12 @@ def student(cdf, nu, corr_matrix):
 def gaussian(cdf, corr_matrix):
     """copulas/gaussian/gaussian.py:43-117."""
     u = np.asarray(cdf, dtype=np.float64)
-    P, d = u.shape
-    z = N.special("ndtri", u)
+    return gaussian_from_quantiles(N.special("ndtri", u), corr_matrix)
+
+
+def gaussian_from_quantiles(z, corr_matrix):
+    """gaussian.py:52-61 after the norm.ppf step."""
+    P, d = z.shape
     Ri, det = np.linalg.inv(corr_matrix), np.linalg.det(corr_matrix)
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
         qf = np.einsum("pi,ij,pj->p", z, Ri, z)
