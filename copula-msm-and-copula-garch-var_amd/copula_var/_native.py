@@ -84,10 +84,12 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_msm_filter": (i32, [i32, i32, d, d, d, d, v, i64, i64, v, i32]),
         "cvq_garch_forecast": (i32, [i32, d, d, d, v, i64, i64, v, i32]),
         "cvq_ukf_forecast": (i32, [i32, d, d, d, v, i64, i64, v, i32]),
+        "cvq_garch_forecast_pq": (i32, [i32, i32, i32, v, v, i64, i64, v, i32]),
         "cvq_msm_loglik": (i32, [i32, i32, v, i64, v, i64, v, i32]),
         "cvq_garch_loglik": (i32, [i32, v, i64, v, i64, v, i32]),
         "cvq_garch_loglik_pq": (i32, [i32, i32, i32, v, i64, v, i64, v, i32]),
         "cvq_ukf_loglik": (i32, [i32, v, i64, v, i64, v, i32]),
+        "cvq_ukf_filter": (i32, [i32, v, i64, v, i32, i64, v, v, i32]),
         "cvq_special": (i32, [i32, i32, d, v, i64, v, i32]),
     }
     for name, (res, args) in sig.items():

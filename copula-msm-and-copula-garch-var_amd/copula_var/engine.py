@@ -198,6 +198,18 @@ def garch_forecast(returns_c, n_in: int, omega: float, alpha: float, beta: float
     return out
 
 
+def garch_forecast_pq(returns_c, n_in: int, p: int, q: int, params, device: int = 0) -> np.ndarray:
+    """GARCH(p, q) sigma forecasts per window; params = (omega, alpha_1..p, beta_1..q)."""
+    r, prm = N.f64(returns_c), N.f64(params).ravel()
+    if prm.size != 1 + p + q:
+        raise ValueError(f"GARCH({p},{q}) needs {1 + p + q} parameters, got {prm.size}")
+    T = r.size - n_in + 1
+    out = np.empty(T)
+    N.check(N.lib().cvq_garch_forecast_pq(device, int(p), int(q), N.ptr(prm), N.ptr(r), n_in, T, N.ptr(out),
+                                          N.MEM_HOST), "cvq_garch_forecast_pq")
+    return out
+
+
 def ukf_forecast(returns_c, n_in: int, a: float, l: float, q: float, device: int = 0) -> np.ndarray:
     r = N.f64(returns_c)
     T = r.size - n_in + 1
@@ -244,3 +256,19 @@ def ukf_loglik(returns, params, device: int = 0) -> np.ndarray:
     N.check(N.lib().cvq_ukf_loglik(device, N.ptr(p), p.shape[0], N.ptr(r), r.size, N.ptr(out), N.MEM_HOST),
             "cvq_ukf_loglik")
     return out
+
+
+def ukf_filter(returns, params, device: int = 0):
+    """params (B, 3) rows (a, l, q); returns (N,) shared or (B, N) one series per row
+    -> (LL (B,), state paths (B, N)); a failed pass has LL -1e10 and a NaN path
+    (estimate.py:270-271: state_estimation None)."""
+    r, p = N.f64(returns), N.f64(np.atleast_2d(params))
+    B = p.shape[0]
+    per = int(r.ndim == 2)
+    if per and r.shape[0] != B:
+        raise ValueError(f"returns has {r.shape[0]} series for {B} parameter rows")
+    n = r.shape[-1]
+    ll, states = np.empty(B), np.empty((n, B))
+    N.check(N.lib().cvq_ukf_filter(device, N.ptr(p), B, N.ptr(r), per, n, N.ptr(ll), N.ptr(states), N.MEM_HOST),
+            "cvq_ukf_filter")
+    return ll, np.ascontiguousarray(states.T)

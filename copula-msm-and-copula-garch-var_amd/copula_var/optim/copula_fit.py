@@ -108,6 +108,10 @@ class StudentCopulaOptimizer(_IFM):
                 print(f"Negative Log-Likelihood for nu={nu}: {nll_corr}")
             if nll_corr < best_nll:
                 best_nll, best_corr_params = nll_corr, res_corr.x
+        if best_corr_params is None:
+            # the reference goes on with None and fails in np.hstack / construct_correlation_matrix
+            raise ValueError("Student copula fit: the negative log-likelihood is NaN for every nu "
+                             "(a marginal at exactly 0 or 1 has an infinite t quantile, student.py:133-172)")
         res_nu = minimize(fun=lambda v: self.negative_log_likelihood(np.hstack((v, best_corr_params))), x0=[10],
                           method=method, bounds=nu_bounds, tol=self.tol, options={"maxiter": self.max_iter})
         optimized_nu = np.array([res_nu.x[0]])

@@ -120,7 +120,9 @@ def sigma_integration_params(centred: np.ndarray, n_in: int, model: str, params:
     dim = centred.shape[1]
     sig = np.empty((centred.shape[0] - n_in, dim))
     for d, p in enumerate(params):
-        if model == "garch":
+        if model == "garch" and "pq" in p:
+            sig[:, d] = engine.garch_forecast_pq(centred[:-1, d], n_in, p["pq"][0], p["pq"][1], p["params"], device)
+        elif model == "garch":
             sig[:, d] = engine.garch_forecast(centred[:-1, d], n_in, p["omega"], p["alpha"], p["beta"], device)
         else:
             sig[:, d] = engine.ukf_forecast(centred[:-1, d], n_in, p["a"], p["l"], p["q"], device)

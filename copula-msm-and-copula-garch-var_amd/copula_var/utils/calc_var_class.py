@@ -48,8 +48,8 @@ class ValueAtRiskCalcualtion:
 
         self.in_sample_params = self.retrieve_param_in_sample(*args, **kwargs)
         self.marginals, self.densities, self.vol_states_array = self.calc_marg_and_densities(*args, **kwargs)
-        self.copula_params = (np.atleast_1d(np.asarray(copula_params, dtype=np.float64))
-                              if copula_params is not None else self.calc_copula_params())
+        self.copula_params = np.atleast_1d(np.asarray(
+            copula_params if copula_params is not None else self.calc_copula_params(), dtype=np.float64))
         self.integrations_params_t, self.integrations_params_static, self.grids_generations_params = (
             self.integration_params_retrieval())
 

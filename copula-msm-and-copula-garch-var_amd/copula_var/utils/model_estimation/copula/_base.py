@@ -8,17 +8,16 @@ from __future__ import annotations
 
 from ...calc_var_ABC import VaRCalculationMethod
 
-#: the copula fit (copulas/*/opti.py, IFM) is out of scope
-FIT_OUT_OF_SCOPE = ("the in-sample copula fit (IFM + scipy optimisers) is out of scope; pass "
-                    "copula_params=... to ValueAtRiskCalcualtion (packed as the adapter's "
-                    "copula_integrations_params would return them)")
-
 
 class CopulaAdapter(VaRCalculationMethod):
     copula_kind = ""
 
     def __init__(self, estimation_method):
         self.estimation_method = estimation_method
+
+    @property
+    def device(self) -> int:
+        return int(getattr(self.estimation_method, "device", 0))
 
     @property
     def model_kind(self) -> str:

@@ -4,7 +4,7 @@ from __future__ import annotations
 import numpy as np
 
 from .... import copulas
-from ._base import FIT_OUT_OF_SCOPE, CopulaAdapter
+from ._base import CopulaAdapter
 
 
 class GaussianCopulaVaR(CopulaAdapter):
@@ -20,9 +20,10 @@ class GaussianCopulaVaR(CopulaAdapter):
         corr[np.tril_indices(n, k=-1)] = rho
         return None, corr
 
-    @staticmethod
-    def copula_or_correl_params_insample(marginals, densities):
-        raise NotImplementedError(FIT_OUT_OF_SCOPE)
+    def copula_or_correl_params_insample(self, marginals, densities):
+        """gaussian_estimation.py:25-33: the IFM fit with device norm.ppf quantiles."""
+        from ....optim.copula_fit import GaussianCopulaOptimizer
+        return GaussianCopulaOptimizer(marginals, densities, device=self.device).optimize()
 
     @staticmethod
     def copula_integrations_params(best_g_params):

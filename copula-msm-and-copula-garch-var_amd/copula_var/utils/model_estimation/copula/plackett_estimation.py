@@ -6,7 +6,7 @@ dim != 2 with CVQ_ERR_UNSUPPORTED."""
 from __future__ import annotations
 
 from .... import copulas
-from ._base import FIT_OUT_OF_SCOPE, CopulaAdapter
+from ._base import CopulaAdapter
 
 
 class PlackettCopulaVaR(CopulaAdapter):
@@ -19,7 +19,9 @@ class PlackettCopulaVaR(CopulaAdapter):
 
     @staticmethod
     def copula_or_correl_params_insample(marginals, densities):
-        raise NotImplementedError(FIT_OUT_OF_SCOPE)
+        """plackett_estimation.py:18-26: the IFM fit (closed-form density)."""
+        from ....optim.copula_fit import PlackettCopulaOptimizer
+        return PlackettCopulaOptimizer(marginals, densities).optimize()
 
     @staticmethod
     def copula_integrations_params(best_p_params):

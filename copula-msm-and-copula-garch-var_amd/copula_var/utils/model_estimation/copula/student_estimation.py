@@ -4,15 +4,17 @@ from __future__ import annotations
 import numpy as np
 
 from .... import copulas
-from ._base import FIT_OUT_OF_SCOPE, CopulaAdapter
+from ._base import CopulaAdapter
 
 
 class StudentCopulaVaR(CopulaAdapter):
     copula_kind = "student"
 
-    @staticmethod
-    def copula_or_correl_params_insample(marginals, densities):
-        raise NotImplementedError(FIT_OUT_OF_SCOPE)
+    def copula_or_correl_params_insample(self, marginals, densities):
+        """student_estimation.py:12-20: copulas/student/opti.py's IFM fit, each objective's
+        t.ppf quantiles in one device launch (optim.copula_fit)."""
+        from ....optim.copula_fit import StudentCopulaOptimizer
+        return StudentCopulaOptimizer(marginals, densities, device=self.device).optimize()
 
     @staticmethod
     def copula_integrations_params(best_t_params):

@@ -10,7 +10,9 @@ falls below 1e-10 makes the reference return None and crash in np.exp
 """
 from __future__ import annotations
 
-from .... import tables
+import numpy as np
+
+from .... import insample, tables
 from ....data_loader.load_data import centred_series
 from ...calc_var_ABC import SharedCacheCopulaMRVaR, VaRCalculationMethod
 from .garch_estimation import GarchEstimation
@@ -20,22 +22,39 @@ class MeanRevertingEstimation(VaRCalculationMethod):
     model_kind = "mean_reverting"
     device = 0
 
-    @staticmethod
-    def model_params_insample(in_sample_dict):
-        """mean_reverting_estimation.py:17-57: cached {'optimal_params': {'a','l','q'}} per
-        ticker (the EM optimiser, kalman_mean_reverting/optimize.py, is out of scope)."""
-        results = {}
-        for ticker in in_sample_dict:
-            if ticker not in SharedCacheCopulaMRVaR.cache:
-                raise NotImplementedError(
-                    f"no in-sample mean-reverting parameters for {ticker!r}: the in-sample optimiser is out "
-                    "of scope; inject them into SharedCacheCopulaMRVaR.cache[ticker]")
-            results[ticker] = SharedCacheCopulaMRVaR.cache[ticker]
-        return results
+    seed = 0
 
-    @staticmethod
-    def calculate_marginals_and_densities_in_sample(in_sample_dict, in_sample_params):
-        return None, None, None
+    def model_params_insample(self, in_sample_dict):
+        """mean_reverting_estimation.py:17-57: {'optimal_params': {'a','l','q'}} per ticker
+        from SharedCacheCopulaMRVaR.cache, else the EM fit (optim.ukf.VolOptimizer(0.99, 0.5,
+        0.1, max_iter=1000, tol=1e-6), :41-47); the uncached tickers' chains run in lockstep,
+        one device UKF launch per round for all of them.  Seeds: self.seed + i."""
+        from ....optim.ukf import VolOptimizer, em_lockstep
+        todo = [t for t in in_sample_dict if t not in SharedCacheCopulaMRVaR.cache]
+        if todo:
+            opts = [VolOptimizer(0.99, 0.5, 0.1, max_iter=1000, tol=1e-6, seed=self.seed + i, device=self.device)
+                    for i in range(len(todo))]
+            fits = em_lockstep(opts, [np.asarray(in_sample_dict[t], dtype=np.float64) for t in todo])
+            for t, (params, _ll) in zip(todo, fits):
+                SharedCacheCopulaMRVaR.cache[t] = {
+                    "optimal_params": {"a": params[0], "l": params[1], "q": params[2]}}
+        return {t: SharedCacheCopulaMRVaR.cache[t] for t in in_sample_dict}
+
+    def calculate_marginals_and_densities_in_sample(self, in_sample_dict, in_sample_params):
+        """mean_reverting_estimation.py:59-119: per ticker (cached under (ticker, 'marginals'))
+        Phi / phi of eps = r / exp(UKF state path) (estimate.py:46-51), stacked (N, dim)."""
+        marg, dens = [], []
+        for ticker, params in in_sample_params.items():
+            key = (ticker, "marginals")
+            if key not in SharedCacheCopulaMRVaR.cache:
+                op = params["optimal_params"]
+                m, d = insample.mr_marginals_densities(np.asarray(in_sample_dict[ticker], dtype=np.float64),
+                                                       op["a"], op["l"], op["q"], self.device)
+                SharedCacheCopulaMRVaR.cache[key] = {"marginals": m, "densities": d}
+            c = SharedCacheCopulaMRVaR.cache[key]
+            marg.append(np.asarray(c["marginals"]).reshape(-1, 1))
+            dens.append(np.asarray(c["densities"]).reshape(-1, 1))
+        return np.hstack(marg), np.hstack(dens), None
 
     def copula_or_correl_params_insample(self, *args, **kwargs):
         raise NotImplementedError("the copula adapter fits the copula")

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .... import tables
+from .... import insample, tables
 from ....data_loader.load_data import centred_series
 from ...calc_var_ABC import SharedCacheCopulaMSMVaR, VaRCalculationMethod
 
@@ -26,29 +26,41 @@ class MSMEstimation(VaRCalculationMethod):
     model_kind = "msm"
     device = 0
 
-    @staticmethod
-    def model_params_insample(in_sample_dict, k):
-        """msm_estimation.py:17-52: cached params per (ticker, k).  The basin-hopping
-        optimiser (markov_switching_multifractal/opti.py) is out of scope:
-        inject {'optimal_params': {'m_0','sig','b','gamma'}} into SharedCacheCopulaMSMVaR.cache."""
+    seed = 0
+
+    def model_params_insample(self, in_sample_dict, k):
+        """msm_estimation.py:17-52: params per (ticker, k) from SharedCacheCopulaMSMVaR.cache,
+        else the basin-hopping fit (optim.msm.Optimizer: the 10 b-chains' proposals in one
+        device launch per iteration; seeded, see optim/msm.py) and cached."""
+        from ....optim.msm import Optimizer
         results = {}
-        for ticker in in_sample_dict:
+        for ticker, returns in in_sample_dict.items():
             key = (ticker, k)
             if key not in SharedCacheCopulaMSMVaR.cache:
-                raise NotImplementedError(
-                    f"no in-sample MSM parameters for {key}: the in-sample optimiser is out of scope; "
-                    "inject them into SharedCacheCopulaMSMVaR.cache[(ticker, k)]")
+                p = Optimizer(np.asarray(returns, dtype=np.float64), k, seed=self.seed, device=self.device).optimize()
+                SharedCacheCopulaMSMVaR.cache[key] = {
+                    "optimal_params": {"m_0": p[0], "sig": p[3], "b": p[1], "gamma": p[2]}}   # :45-48
             results[ticker] = SharedCacheCopulaMSMVaR.cache[key]
         return results
 
     @staticmethod
     def calculate_marginals_and_densities_in_sample(in_sample_dict, in_sample_params, k):
-        """msm_estimation.py:55-118.  Only vol_states_array (2**k vol states per ticker,
-        calc_prob.py:103-108) feeds the VaR path; the in-sample marginals / densities feed
-        the copula fit, which is out of scope, and are returned as None."""
-        vsa = np.array([tables.msm_vol_states(k, p["optimal_params"]["m_0"], p["optimal_params"]["sig"])
-                        for p in in_sample_params.values()])
-        return None, None, vsa
+        """msm_estimation.py:55-120: per ticker (cached under (ticker, 'marginals_k'))
+        the filtered-probability-weighted normal cdf / pdf of the in-sample returns
+        (calc_marginals.py:7-30), stacked (N-1, dim), and the 2**k vol states."""
+        marg, dens, vs = [], [], []
+        for ticker, params in in_sample_params.items():
+            key = (ticker, f"marginals_{k}")
+            if key not in SharedCacheCopulaMSMVaR.cache:
+                op = params["optimal_params"]
+                m, d, v = insample.msm_marginals_densities(np.asarray(in_sample_dict[ticker], dtype=np.float64), k,
+                                                           op["m_0"], op["sig"], op["b"], op["gamma"])
+                SharedCacheCopulaMSMVaR.cache[key] = {"marginals": m, "densities": d, "vol_states": v}
+            c = SharedCacheCopulaMSMVaR.cache[key]
+            marg.append(np.asarray(c["marginals"]).reshape(-1, 1))
+            dens.append(np.asarray(c["densities"]).reshape(-1, 1))
+            vs.append(c["vol_states"])
+        return np.hstack(marg), np.hstack(dens), np.array(vs)
 
     def copula_or_correl_params_insample(self, *args, **kwargs):
         raise NotImplementedError("the copula adapter fits the copula")

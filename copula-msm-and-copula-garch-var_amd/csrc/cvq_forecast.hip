@@ -245,6 +245,61 @@ __global__ void k_garch_loglik_pq(const double* __restrict__ prm, long long B, c
     out[b] = -0.5 * acc;
 }
 
+// GARCH(p, q) calc_forecast (garch/forecast.py:5-19) per window t of n_in returns
+// (one thread per window): the variance recursion above, then
+// sqrt((omega + sum_i alpha_i r[n-p+i]^2) + sum_j beta_j sigma2[n-q+j]) -- note the
+// reference pairs alpha_1 with the OLDEST of the last p returns (returns[-p:]).
+template <int P, int Q>
+__global__ void k_garch_forecast_pq(const double* __restrict__ prm, const double* __restrict__ r, long long n_in,
+                                    long long T, double* __restrict__ out) {
+    const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 >= T) return;
+    const double* w = r + t0;
+    const double omega = prm[0];
+    double alpha[P], beta[Q], sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) { alpha[i] = prm[1 + i]; sa += alpha[i]; }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) { beta[j] = prm[1 + P + j]; sb += beta[j]; }
+    double hist[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) hist[j] = 0.0;
+    hist[0] = omega / (1 - sa - sb);
+    for (long long t = 1; t < n_in; ++t) {
+        double v = omega;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (i < t) v += alpha[i] * (w[t - i - 1] * w[t - i - 1]);
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+            if (j < t) v += beta[j] * hist[j];
+        const double s2 = (v < 1e-7) ? 1e-7 : v;
+#pragma unroll
+        for (int j = Q - 1; j > 0; --j) hist[j] = hist[j - 1];
+        hist[0] = s2;
+    }
+    double s_a = 0.0, s_b = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const double ri = w[n_in - P + i];
+        s_a = (i == 0) ? alpha[i] * (ri * ri) : s_a + alpha[i] * (ri * ri);
+    }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) s_b = (j == 0) ? beta[j] * hist[Q - 1] : s_b + beta[j] * hist[Q - 1 - j];
+    out[t0] = sqrt((omega + s_a) + s_b);
+}
+
+template <int P>
+void launch_garch_forecast_pq(int q, const double* prm, const double* r, long long n_in, long long T, double* o) {
+    const dim3 g((unsigned)((T + 255) / 256)), blk(256);
+    switch (q) {
+        case 1: hipLaunchKernelGGL((k_garch_forecast_pq<P, 1>), g, blk, 0, 0, prm, r, n_in, T, o); break;
+        case 2: hipLaunchKernelGGL((k_garch_forecast_pq<P, 2>), g, blk, 0, 0, prm, r, n_in, T, o); break;
+        case 3: hipLaunchKernelGGL((k_garch_forecast_pq<P, 3>), g, blk, 0, 0, prm, r, n_in, T, o); break;
+        default: hipLaunchKernelGGL((k_garch_forecast_pq<P, 4>), g, blk, 0, 0, prm, r, n_in, T, o); break;
+    }
+}
+
 template <int P>
 void launch_garch_pq(int q, const double* p, long long B, const double* r, long long N, double* o) {
     const dim3 g((unsigned)((B + 63) / 64)), blk(64);
@@ -275,9 +330,11 @@ UkfConst ukf_const(double alpha = 1.6, double beta = 2.0, double kappa = 1.75) {
     return c;
 }
 
-// Runs one UKF pass; returns false on the Z < 1e-10 failure (estimate.py:219-220).
+// Runs one UKF pass; returns false on the Z < 1e-10 failure (estimate.py:219-220) or a
+// NaN mean / variance / Z (:270-271).  states != nullptr: the filtered means
+// (state_estimation, :273) are written with stride `sstride`.
 __device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const double* w, long long N,
-                         double* xmean_last, double* LL) {
+                         double* xmean_last, double* LL, double* states = nullptr, long long sstride = 1) {
     double x = l, var = q;                                        // forecast.py:9: init (l, q)
     double xm = 0.0, ll = 0.0;
     for (long long t = 0; t < N; ++t) {
@@ -310,6 +367,8 @@ __device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const 
             const double d = X2[i] - mean;
             v2 += (i == 0 ? C.wm2_0 : C.wm2_1) * ((h[i] / Z) * (d * d));
         }
+        if (isnan(mean) || isnan(v2) || isnan(Z)) return false;
+        if (states) states[t * sstride] = mean;
         ll += log(fabs(Z));
         x = mean;
         var = v2;
@@ -339,6 +398,23 @@ __global__ void k_ukf_loglik(UkfConst C, const double* __restrict__ prm, long lo
     double xm, ll;
     const bool ok = ukf_pass(C, prm[3 * b], prm[3 * b + 1], prm[3 * b + 2], r, N, &xm, &ll);
     out[b] = ok ? ll : -1e10;                                     // estimate.py:270-271
+}
+
+// KalmanFilterVolEstimation (estimate.py:7-51, init (l, q) as VolOptimizer.e_step,
+// kalman_mean_reverting/optimize.py:28-32): LL and the filtered state path of each
+// candidate.  Path layout [N][B] (time-major) so the B candidates' stores coalesce;
+// a failed pass leaves LL = -1e10 and NaN in its column (state_estimation None).
+__global__ void k_ukf_filter(UkfConst C, const double* __restrict__ prm, long long B, const double* __restrict__ r,
+                             long long r_stride, long long N, double* __restrict__ ll_out,
+                             double* __restrict__ states) {
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xm, ll;
+    const bool ok = ukf_pass(C, prm[3 * b], prm[3 * b + 1], prm[3 * b + 2], r + b * r_stride, N, &xm, &ll,
+                             states + b, B);
+    ll_out[b] = ok ? ll : -1e10;
+    if (!ok)
+        for (long long t = 0; t < N; ++t) states[t * B + b] = __builtin_nan("");
 }
 
 // ------------------------------------------------------------------ KAT
@@ -462,6 +538,35 @@ int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double be
     return finish_out(out, T, mem, dout);
 }
 
+int32_t cvq_garch_forecast_pq(int32_t device, int32_t p, int32_t q, const double* params, const double* returns_c,
+                              int64_t n_in, int64_t T, double* out, int32_t mem) {
+    CVQ_REQUIRE(params && returns_c && out && n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "bad argument");
+    CVQ_REQUIRE(p >= 1 && q >= 1 && p <= kGarchMaxPQ && q <= kGarchMaxPQ, CVQ_ERR_UNSUPPORTED,
+                "GARCH orders must be 1 <= p, q <= 4");
+    CVQ_REQUIRE(n_in >= p && n_in >= q, CVQ_ERR_INVALID, "window shorter than the GARCH order");
+    double s = 0.0;
+    bool pos = params[0] > 0;
+    for (int i = 1; i <= p + q; ++i) { pos = pos && params[i] > 0; s += params[i]; }
+    CVQ_REQUIRE(pos && s < 1, CVQ_ERR_INVALID,
+                "GARCH parameters must be positive with sum(alpha) + sum(beta) < 1 (garch/estimation.py:22-38)");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DevBuf pin, rin, dout;
+    const double *d_p, *d_r;
+    double* d_out;
+    // params always come from host memory (1 + p + q doubles)
+    if ((rc = stage_in(params, 1 + p + q, CVQ_MEM_HOST, pin, &d_p)) ||
+        (rc = stage_in(returns_c, n_in + T - 1, mem, rin, &d_r)) || (rc = stage_out(out, T, mem, dout, &d_out)))
+        return rc;
+    switch (p) {
+        case 1: launch_garch_forecast_pq<1>(q, d_p, d_r, n_in, T, d_out); break;
+        case 2: launch_garch_forecast_pq<2>(q, d_p, d_r, n_in, T, d_out); break;
+        case 3: launch_garch_forecast_pq<3>(q, d_p, d_r, n_in, T, d_out); break;
+        default: launch_garch_forecast_pq<4>(q, d_p, d_r, n_in, T, d_out); break;
+    }
+    return finish_out(out, T, mem, dout);
+}
+
 int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q, const double* returns_c, int64_t n_in,
                          int64_t T, double* out, int32_t mem) {
     CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
@@ -575,6 +680,27 @@ int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B, const do
     hipLaunchKernelGGL(k_ukf_loglik, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, 0, ukf_const(), d_p, B, d_r, N,
                        d_out);
     return finish_out(out, B, mem, dout);
+}
+
+int32_t cvq_ukf_filter(int32_t device, const double* params, int64_t B, const double* returns, int32_t per_candidate,
+                       int64_t N, double* ll_out, double* states_out, int32_t mem) {
+    CVQ_REQUIRE(params && returns && ll_out && states_out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
+    int rc = check_device(device);
+    if (rc) return rc;
+    const long long r_stride = per_candidate ? N : 0;
+    DevBuf pin, rin, dll, dst;
+    const double *d_p, *d_r;
+    double *d_ll, *d_st;
+    if ((rc = stage_in(params, (size_t)B * 3, mem, pin, &d_p)) ||
+        (rc = stage_in(returns, per_candidate ? (size_t)B * N : (size_t)N, mem, rin, &d_r)) ||
+        (rc = stage_out(ll_out, B, mem, dll, &d_ll)) || (rc = stage_out(states_out, (size_t)B * N, mem, dst, &d_st)))
+        return rc;
+    hipLaunchKernelGGL(k_ukf_filter, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, 0, ukf_const(), d_p, B, d_r,
+                       r_stride, N, d_ll, d_st);
+    if ((rc = finish_out(ll_out, B, mem, dll))) return rc;
+    if (mem != CVQ_MEM_DEVICE)
+        CVQ_HIP_CHECK(hipMemcpy(states_out, dst.p, (size_t)B * N * sizeof(double), hipMemcpyDeviceToHost));
+    return CVQ_OK;
 }
 
 int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int64_t n, double* out, int32_t mem) {

@@ -155,6 +155,10 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
  * out [T] = sigma forecast per window. */
 int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double beta,
                            const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
+/* GARCH(p, q) compute_forecast, 1 <= p, q <= 4 (garch/forecast.py:5-19):
+ * params (host) [1 + p + q] = (omega, alpha_1..p, beta_1..q); out [T]. */
+int32_t cvq_garch_forecast_pq(int32_t device, int32_t p, int32_t q, const double* params, const double* returns_c,
+                              int64_t n_in, int64_t T, double* out, int32_t mem);
 /* UKF compute_forecast (mean_reverting_estimation.py:192-232 -> forecast.py:5-12 ->
  * estimate.py:230-281); Q19 semantics.  out [T]. */
 int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q,
@@ -174,6 +178,14 @@ int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B,
 /* GARCH(p, q), 1 <= p, q <= 4, for the (p, q) search of GarchOptimizer.optimize
  * (garch/opti.py:89-137): params [B][1 + p + q] = (omega, alpha_1..p, beta_1..q);
  * garch/estimation.py:91-125 incl. the max(p, q) chopped prefix. */
+/* UKF E-step of VolOptimizer (kalman_mean_reverting/optimize.py:28-32 ->
+ * estimate.py:7-51, 230-281): per candidate (a, l, q) [B][3] the log-likelihood
+ * ll_out [B] (-1e10 on the Z / NaN failure) and the filtered state path
+ * states_out [N][B] (time-major; NaN column on failure).  returns: one series [N]
+ * shared by all candidates (per_candidate = 0) or one per candidate [B][N]
+ * (per_candidate = 1: several assets' EM chains in one launch). */
+int32_t cvq_ukf_filter(int32_t device, const double* params, int64_t B, const double* returns, int32_t per_candidate,
+                       int64_t N, double* ll_out, double* states_out, int32_t mem);
 int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* params, int64_t B,
                             const double* returns, int64_t N, double* out, int32_t mem);
 

@@ -76,6 +76,17 @@ def test_student_optimizer_two_stage(sample2):
     assert min(abs(res["optimized_params"][1] - s[0]) for s in sweep) < 1e-5
 
 
+def test_student_optimizer_all_nan_objective_raises(sample2):
+    """A marginal at exactly 1 gives t.ppf = inf and a NaN objective for every nu; the
+    reference then fails on best_corr_params None -- here a ValueError says why."""
+    from copula_var.optim.copula_fit import Optimizer
+    u, d = sample2
+    u = u.copy()
+    u[0, 0] = 1.0
+    with pytest.raises(ValueError, match="NaN for every nu"):
+        Optimizer(u, d, nu_values=np.array([4.0]), tppf=_tppf).optimize()
+
+
 @pytest.mark.parametrize("rho", [0.2, 0.7, -0.5, 0.99, 1.0])
 def test_gaussian_nll_matches_oracle(sample2, rho):
     from oracle.copula_fit import gaussian_nll

@@ -76,16 +76,31 @@ def test_copula_parameter_packing():
     assert PlackettCopulaVaR.unpack_copula_params(3.0) == (3.0, None)
 
 
-def test_out_of_scope_stages_raise_clearly():
+def test_insample_stages_use_the_caches_then_the_device():
+    """model_params_insample: the reference's cache first (msm_estimation.py:35-38); a miss
+    runs the device-batched optimiser, which fails loudly without a GPU.  The in-sample
+    marginals (host filter) are cached under the reference's key."""
+    from copula_var import _native as N
     from copula_var.utils.factory import ValueAtRiskCalculationFactory as F
     from copula_var.utils.calc_var_ABC import SharedCacheCopulaMSMVaR
     SharedCacheCopulaMSMVaR.cache.clear()
     c = F.create_var_calculator(copula_type="student", estimation_type="msm")
-    with pytest.raises(NotImplementedError, match="out of scope"):
-        c.model_params_insample({"A": np.zeros(3)}, k=4)
-    with pytest.raises(NotImplementedError, match="copula fit"):
-        c.copula_or_correl_params_insample(None, None)
+    if not _gpu():
+        with pytest.raises(N.NativeError):
+            c.model_params_insample({"A": np.linspace(-1, 1, 50)}, k=4)
     SharedCacheCopulaMSMVaR.cache[("A", 4)] = {"optimal_params": {"m_0": 0.45, "sig": 1.2, "b": 3.0, "gamma": 0.3}}
-    got = c.model_params_insample({"A": np.zeros(3)}, k=4)
-    _, _, vsa = c.calculate_marginals_and_densities_in_sample({"A": np.zeros(3)}, got, k=4)
-    assert vsa.shape == (1, 16)
+    r = np.linspace(-2, 2, 40)
+    got = c.model_params_insample({"A": r}, k=4)
+    m, d, vsa = c.calculate_marginals_and_densities_in_sample({"A": r}, got, k=4)
+    assert vsa.shape == (1, 16) and m.shape == d.shape == (39, 1)
+    assert np.all((m > 0) & (m < 1)) and np.all(d > 0)
+    assert ("A", "marginals_4") in SharedCacheCopulaMSMVaR.cache
+    SharedCacheCopulaMSMVaR.cache.clear()
+
+
+def _gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
