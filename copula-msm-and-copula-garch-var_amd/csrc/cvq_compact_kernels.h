@@ -7,9 +7,9 @@
 // the inner-index range (cnt_r(a), cnt_r(b)] with cnt_r(v) = largest j with
 // x_j <= (v - x_r w1) / w0, else 0 (create_grids.py:102-108, Q9/Q10).
 //
-// One NT-thread workgroup per date (NT = 64 by default: one wavefront, so the
-// per-level reductions need no LDS and no barrier); thread tid owns the outer
-// rows tid + NT k.
+// One NT-thread workgroup per date (NT = 256 by default, CVQ_COMPACT_NT; NT = 64
+// -- one wavefront, no LDS reduction or barrier -- measured slower for lack of
+// latency hiding); thread tid owns the outer rows tid + NT k.
 //  1. Tables: thread i evaluates the table entries of grid index i on both axes
 //     (table_entry's arithmetic, the Student quantile written without
 //     data-dependent branches so the two entries' memory latencies overlap) ->
