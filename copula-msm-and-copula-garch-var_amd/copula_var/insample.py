@@ -48,7 +48,7 @@ def msm_state_probs(returns, k, m0, sig, b, gamma):
     probs = np.zeros((r.size, S))
     prev = np.full(S, 1 / S)
     for i in range(r.size):
-        trans = np.array([np.sum(A[j, :] * prev) for j in range(S)])            # :56-57
+        trans = A @ prev                                                        # :56-57
         p = trans * cond[i]
         scale = np.sum(p)
         if scale == 0:
