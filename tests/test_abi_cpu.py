@@ -77,6 +77,26 @@ def test_host_side_validation_without_gpu():
     assert 20 <= s.value <= 30
 
 
+def test_in_sample_entry_points_validate_on_the_host():
+    """GARCH(p, q) forecast / likelihood and the UKF E-step reject bad orders, GARCH
+    parameters that garch/estimation.py:22-38 rejects, and NULL buffers before any HIP call."""
+    import numpy as np
+    from copula_var import _native as N
+    lib = N.lib()
+    r, out = np.zeros(50), np.zeros(50)
+    ok = np.array([0.05, 0.1, 0.05, 0.6])                                  # (p, q) = (2, 1)
+    bad = np.array([0.05, 0.5, 0.3, 0.4])                                  # sum >= 1
+    neg = np.array([0.05, -0.1, 0.05, 0.6])
+    f = lambda p, q, prm: lib.cvq_garch_forecast_pq(0, p, q, N.ptr(prm), N.ptr(r), 10, 5, N.ptr(out), N.MEM_HOST)
+    assert f(2, 1, bad) == N.CVQ_ERR_INVALID
+    assert f(2, 1, neg) == N.CVQ_ERR_INVALID
+    assert f(5, 1, np.zeros(7) + 0.01) == N.CVQ_ERR_UNSUPPORTED
+    assert lib.cvq_garch_loglik_pq(0, 0, 1, N.ptr(ok), 1, N.ptr(r), 50, N.ptr(out), N.MEM_HOST) == \
+        N.CVQ_ERR_UNSUPPORTED
+    assert lib.cvq_ukf_filter(0, None, 1, N.ptr(r), 0, 50, N.ptr(out), N.ptr(out), N.MEM_HOST) == N.CVQ_ERR_INVALID
+    assert lib.cvq_last_error()
+
+
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     """No CPU fallback: a missing libcvq.so raises instead of computing."""
     import importlib
