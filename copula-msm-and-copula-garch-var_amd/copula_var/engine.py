@@ -61,9 +61,9 @@ class QuadraturePlan:
         st.copula_params = dp(self._cp)
         st.n_copula_params = self._cp.size
         if strategy == "auto":                          # DIRECT / COMPACT are built for 2 assets
-            strategy = "compact" if self.dim == 2 else "prefix"
+            strategy = "compact" if self.dim == 2 else "sorted"
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
-                       "compact": N.STRATEGY_COMPACT}[strategy]
+                       "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED}[strategy]
         self.strategy = strategy
         st.v_cap = float(v_cap)
         self._static = st

@@ -294,6 +294,48 @@ __device__ __forceinline__ void table_pair(const StaticDev& S, const double* __r
 template <int NT>
 constexpr int kWtotInts = ((NT / 64) + 3) & ~3;
 
+// k_finalize for a single rank, run by the last workgroup of a solve launch over
+// T dates (calc_var_class.py:278, :293, :171): Q2 / Q4 from the header, VaR =
+// snapshot + ptf_mean, status words to P.fin_err, header and ticket reset for
+// the next launch.
+template <int NT>
+__device__ __forceinline__ void fused_finalize(const SolveConst& P, Header* hdr, const double* __restrict__ snaps,
+                                               long long T) {
+    const int tid = threadIdx.x;
+    __threadfence();                                     // acquire: every workgroup's stores
+    const int Nit = __hip_atomic_load(&hdr->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int err = __hip_atomic_load(&hdr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (Nit > P.K ? 2 : 0);
+    const unsigned long long nz = __hip_atomic_load((unsigned long long*)&hdr->nonzero, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    int kstop = min(Nit, P.K);
+    for (int k = 0; k < kstop; ++k)
+        if (!((nz >> k) & 1ull)) { kstop = k; break; }
+    // every load in flight before the first store: one memory latency for T <= 4 NT
+    for (long long d0 = tid; d0 < T; d0 += 4 * NT) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            v[u] = d < T ? snaps[d * P.stride + kstop] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long d = d0 + (long long)u * NT;
+            if (d < T) P.fin_var[d] = v[u] + P.ptf_mean;
+        }
+    }
+    __syncthreads();                                     // every thread has read the header
+    if (tid == 0) {
+        P.fin_err[0] = err;
+        P.fin_err[1] = kstop;
+        P.fin_err[2] = Nit;
+        P.fin_err[3] = 0;                                // ticket reset for the next launch
+        hdr->iters = 0;                                  // header reset for the next launch
+        hdr->error = 0;
+        hdr->nonzero = 0;
+    }
+}
+
 // ------------------------------------------------------------------ the kernel
 // calc_var solve: snapshots + header, fused finalize when P.fin_var.
 // Thread tid owns rows tid + NT k (k < RPT, RPT = ceil(n / NT)); NT = 64 makes the
@@ -610,39 +652,7 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     if (!P.fin_var) return;
     __syncthreads();
     if (!last) return;
-    // k_finalize for a single rank, run by the last workgroup (calc_var_class.py:278, :293, :171)
-    __threadfence();                                     // acquire: every workgroup's stores
-    const int Nit = __hip_atomic_load(&hdr->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int err = __hip_atomic_load(&hdr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (Nit > P.K ? 2 : 0);
-    const unsigned long long nz = __hip_atomic_load((unsigned long long*)&hdr->nonzero, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-    int kstop = min(Nit, P.K);
-    for (int k = 0; k < kstop; ++k)
-        if (!((nz >> k) & 1ull)) { kstop = k; break; }
-    // every load in flight before the first store: one memory latency for T <= 4 NT
-    for (long long d0 = tid; d0 < (long long)gridDim.x; d0 += 4 * NT) {
-        double v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const long long d = d0 + (long long)u * NT;
-            v[u] = d < (long long)gridDim.x ? snaps[d * P.stride + kstop] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const long long d = d0 + (long long)u * NT;
-            if (d < (long long)gridDim.x) P.fin_var[d] = v[u] + P.ptf_mean;
-        }
-    }
-    __syncthreads();                                     // every thread has read the header
-    if (tid == 0) {
-        P.fin_err[0] = err;
-        P.fin_err[1] = kstop;
-        P.fin_err[2] = Nit;
-        P.fin_err[3] = 0;                                // ticket reset for the next launch
-        hdr->iters = 0;                                  // header reset for the next launch
-        hdr->error = 0;
-        hdr->nonzero = 0;
-    }
+    fused_finalize<NT>(P, hdr, snaps, (long long)gridDim.x);
 }
 
 // LDS bytes of one k_compact workgroup

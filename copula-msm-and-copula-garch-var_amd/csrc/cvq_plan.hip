@@ -15,6 +15,7 @@
 #include "cvq_quad_kernels.h"
 #include "cvq_direct_kernels.h"
 #include "cvq_compact_kernels.h"
+#include "cvq_sorted_kernels.h"
 #include "cvq_tppf_tables.h"
 
 namespace cvq {
@@ -154,6 +155,16 @@ struct cvq_plan {
     int16_t* d_cutfix = nullptr; // [n][kCutFixed]
     double cut_key[6] = {0, 0, 0, 0, 0, 0};
     bool cut_valid = false;
+    // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
+    // ub() of the fixed levels and the bisection trees for the cached solve arguments
+    std::vector<double> hvs;
+    uint32_t* d_sidx = nullptr;  // [G]
+    double* d_svs = nullptr;     // [G]
+    int* d_tree = nullptr;       // [4][1 << tree_depth]
+    int tree_depth = 0;
+    int fixpos[6] = {0, 0, 0, 0, 0, 0};
+    double tree_key[7] = {0, 0, 0, 0, 0, 0, 0};
+    bool tree_valid = false;
     long long capStamps = 0;
     // optional per-kernel timing (HIP events on the plan's stream)
     int timing = 0;              // bitmask of kernel kinds timed with HIP events
@@ -355,23 +366,112 @@ inline double o2d(int64_t o) {
 // v*(r, j): the smallest double v with x_j <= (v - lev_r) / w0, the exact FP64
 // membership rule of the nested grid (Q10): node (r, j >= 1) lies in the slab
 // (a, b] iff a < v* <= b, because (v - lev) / w0 is non-decreasing in v.
+double vstar_exact(double xj, double lev, double w0) {
+    auto pred = [&](double v) { return xj <= (v - lev) / w0; };
+    double v = xj * w0 + lev;                                  // within a few ulps of v*
+    int steps = 0;
+    if (pred(v)) {
+        for (double d; steps < 64 && pred(d = std::nextafter(v, -HUGE_VAL)); ++steps) v = d;
+    } else {
+        for (; steps < 64 && !pred(v); ++steps) v = std::nextafter(v, HUGE_VAL);
+    }
+    if (steps < 64) return v;
+    int64_t lo = d2o(-HUGE_VAL), hi = d2o(HUGE_VAL);           // pred(lo) false, pred(hi) true
+    while (hi - lo > 1) {
+        const int64_t m = lo + (hi - lo) / 2;
+        if (pred(o2d(m))) hi = m; else lo = m;
+    }
+    return o2d(hi);
+}
+
 void build_vstar(const std::vector<double>& x, double w0, double w1, std::vector<double>& out) {
     const int n = (int)x.size();
     out.assign((size_t)n * n, 0.0);
     for (int r = 0; r < n; ++r) {
         const double lev = x[r] * w1;                          // integration_algo.py:20 (2-D)
-        for (int j = 0; j < n; ++j) {
-            auto pred = [&](double v) { return x[j] <= (v - lev) / w0; };
-            const double g = x[j] * w0 + lev, h = 1e-9 * (std::fabs(g) + 1.0);
-            int64_t lo = d2o(g - h), hi = d2o(g + h);          // pred(lo) false, pred(hi) true
-            if (pred(o2d(lo)) || !pred(o2d(hi))) { lo = d2o(-HUGE_VAL); hi = d2o(HUGE_VAL); }
-            while (hi - lo > 1) {
-                const int64_t m = lo + (hi - lo) / 2;
-                if (pred(o2d(m))) hi = m; else lo = m;
+        for (int j = 0; j < n; ++j) out[(size_t)r * n + j] = vstar_exact(x[j], lev, w0);
+    }
+}
+
+// SORTED: every reachable node (row r, inner j in [1, kmax_r]) with its v*, sorted
+// by (v*, packed index); packed = i0 | j << 16 (2-D), i0 | i1 << 8 | j << 16 (3-D).
+void build_sorted_nodes(const std::vector<double>& x, const StaticDev& S, const std::vector<int>& kmax,
+                        std::vector<double>& vs, std::vector<uint32_t>& idx) {
+    const int n = S.n;
+    std::vector<std::pair<double, uint32_t>> nodes;
+    nodes.reserve((size_t)S.G);
+    for (int r = 0; r < S.nrows; ++r) {
+        const int i0 = S.dim == 2 ? r : r / n, i1 = S.dim == 2 ? 0 : r % n;
+        const double lev = S.dim == 2 ? x[i0] * S.w1 : x[i0] * S.w1 + x[i1] * S.w2;   // integration_algo.py:20
+        const uint32_t base = S.dim == 2 ? (uint32_t)i0 : (uint32_t)(i0 | (i1 << 8));
+        for (int j = 1; j <= kmax[r]; ++j) nodes.emplace_back(vstar_exact(x[j], lev, S.w0), base | ((uint32_t)j << 16));
+    }
+    std::sort(nodes.begin(), nodes.end());
+    vs.resize(nodes.size());
+    idx.resize(nodes.size());
+    for (size_t k = 0; k < nodes.size(); ++k) {
+        vs[k] = nodes[k].first;
+        idx[k] = nodes[k].second;
+    }
+}
+
+int host_ub(const std::vector<double>& vs, double v) {        // #{v* <= v}; NaN -> 0
+    if (!(v == v)) return 0;
+    return (int)(std::upper_bound(vs.begin(), vs.end(), v) - vs.begin());
+}
+
+// ub() of the fixed levels and, per bracket, of the bisection mids down to the depth
+// where every cell holds <= kSortTailCap nodes (the device searches deeper levels).
+int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
+    const double key[7] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax, (double)P.K};
+    if (p->tree_valid && std::memcmp(key, p->tree_key, sizeof key) == 0) return CVQ_OK;
+    const std::vector<double>& vs = p->hvs;
+    for (int e = 0; e < 6; ++e) p->fixpos[e] = host_ub(vs, key[e]);
+    const double br[4][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.sg1, P.vmax}, {P.fg, P.sg1}};   // k_sorted's br
+    const int dmax = std::max(0, std::min(kSortMaxDepth, P.K));
+    std::vector<double> lo, hi;
+    std::vector<int> tree;
+    int depth = dmax;
+    for (int d = 0; d <= dmax; ++d) {                          // cells of depth d: heap nodes [2^d, 2^(d+1))
+        bool small = true;
+        for (int b = 0; b < 4 && small; ++b) {
+            double l = br[b][0], h = br[b][1];
+            for (int h0 = 1 << d, k = 0; k < (1 << d) && small; ++k) {
+                // walk from the root along the path bits of heap node h0 + k
+                const int node = h0 + k;
+                l = br[b][0];
+                h = br[b][1];
+                for (int bit = d - 1; bit >= 0; --bit) {
+                    const double mid = (l + h) / 2;
+                    if ((node >> bit) & 1) l = mid; else h = mid;
+                }
+                if (host_ub(vs, h) - host_ub(vs, l) > kSortTailCap) small = false;
             }
-            out[(size_t)r * n + j] = o2d(hi);
+        }
+        if (small) { depth = d; break; }
+    }
+    tree.assign((size_t)4 << depth, 0);
+    for (int b = 0; b < 4; ++b) {
+        lo.assign((size_t)1 << depth, 0.0);
+        hi.assign((size_t)1 << depth, 0.0);
+        if (depth > 0) { lo[1] = br[b][0]; hi[1] = br[b][1]; }
+        for (int h = 1; h < (1 << depth); ++h) {
+            const double mid = (lo[h] + hi[h]) / 2;            // the device's (lo + hi) / 2
+            tree[((size_t)b << depth) + h] = host_ub(vs, mid);
+            if (2 * h + 1 < (1 << depth)) {
+                lo[2 * h] = lo[h]; hi[2 * h] = mid;
+                lo[2 * h + 1] = mid; hi[2 * h + 1] = hi[h];
+            }
         }
     }
+    p->tree_valid = false;
+    if (int rc = dev_alloc(&p->d_tree, tree.size())) return rc;
+    CVQ_HIP_CHECK(hipMemcpyAsync(p->d_tree, tree.data(), tree.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    p->tree_depth = depth;
+    std::memcpy(p->tree_key, key, sizeof key);
+    p->tree_valid = true;
+    return CVQ_OK;
 }
 
 // Grid lookup buckets: bucket b covers [x_0 + b h, x_0 + (b + 1) h); its entry is
@@ -415,11 +515,30 @@ int compact_max_n();                                                            
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
                    double* snaps, Header* hdr);
+int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
+                  const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
+                  const double* bounds, double* out, double* snaps, Header* hdr);           // cvq_sorted.hip
 }
 namespace {
 
+SortedGeom sorted_geom(const cvq_plan* p) {
+    SortedGeom G{};
+    G.idx = p->d_sidx;
+    G.vs = p->d_svs;
+    G.tree = p->d_tree;
+    G.G = (int)p->S.G;
+    G.depth = p->tree_depth;
+    for (int e = 0; e < 6; ++e) G.fix[e] = p->fixpos[e];
+    return G;
+}
+
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
+    if (p->strategy == CVQ_STRATEGY_SORTED) {
+        if (int rc = ensure_sorted_tree(p, P)) return rc;
+        return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
+                             direct_fused(p), 0, nullptr, nullptr, snaps, hdr);
+    }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
         if (rc) return rc;
@@ -457,6 +576,11 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     TimedScope ts(p, TK_SLAB);
+    if (p->strategy == CVQ_STRATEGY_SORTED) {
+        SolveConst P{};
+        return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
+                             direct_fused(p), 1, bounds, out, nullptr, nullptr);
+    }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {      // COMPACT: slabs of arbitrary bounds run k_direct
         SolveConst P{};
         return launch_direct(p, P, 1, bounds, out, nullptr, nullptr);
@@ -561,6 +685,11 @@ int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
     return CVQ_OK;
 }
 
+// PREFIX and SORTED hold only the nodes with level <= v_cap
+bool materialised(const cvq_plan* p) {
+    return p->strategy == CVQ_STRATEGY_PREFIX || p->strategy == CVQ_STRATEGY_SORTED;
+}
+
 SolveConst solve_const(const cvq_solve_args& a, int K) {
     SolveConst P;
     P.obj = a.obj_var;
@@ -583,7 +712,7 @@ int check_args(const cvq_plan* p, const cvq_solve_args* a) {
     CVQ_REQUIRE(a != nullptr, CVQ_ERR_INVALID, "solve args is NULL");
     const double top = std::max({a->first_guess, a->second_guess_lo, a->second_guess_hi, a->max_var, a->min_var,
                                  a->lower});
-    CVQ_REQUIRE(p->strategy != CVQ_STRATEGY_PREFIX || !(top > p->v_cap), CVQ_ERR_RANGE,
+    CVQ_REQUIRE(!materialised(p) || !(top > p->v_cap), CVQ_ERR_RANGE,
                 "a VaR level in the solve arguments exceeds the plan's v_cap");
     CVQ_REQUIRE(a->tolerance > 0.0, CVQ_ERR_INVALID, "tolerance must be > 0");
     return CVQ_OK;
@@ -658,10 +787,12 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
                 CVQ_ERR_INVALID, "NULL static table");
     CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
     CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
-    CVQ_REQUIRE(s->strategy == CVQ_STRATEGY_PREFIX || s->strategy == CVQ_STRATEGY_DIRECT ||
-                    s->strategy == CVQ_STRATEGY_COMPACT, CVQ_ERR_INVALID, "unknown strategy");
-    CVQ_REQUIRE(!(s->strategy != CVQ_STRATEGY_PREFIX && s->dim != 2), CVQ_ERR_UNSUPPORTED,
-                "the DIRECT and COMPACT strategies are built for dim == 2");
+    CVQ_REQUIRE(s->strategy >= CVQ_STRATEGY_PREFIX && s->strategy <= CVQ_STRATEGY_SORTED, CVQ_ERR_INVALID,
+                "unknown strategy");
+    CVQ_REQUIRE(!((s->strategy == CVQ_STRATEGY_DIRECT || s->strategy == CVQ_STRATEGY_COMPACT) && s->dim != 2),
+                CVQ_ERR_UNSUPPORTED, "the DIRECT and COMPACT strategies are built for dim == 2");
+    CVQ_REQUIRE(!(s->strategy == CVQ_STRATEGY_SORTED && s->dim == 3 && s->n > 255), CVQ_ERR_UNSUPPORTED,
+                "the SORTED strategy supports num_points <= 255 in 3-D");
     for (int l = 0; l < Q; ++l) {             // create_vol_combinations ij order (msm_estimation.py:384)
         int rem = l;
         for (int d = s->dim - 1; d >= 0; --d) {
@@ -790,6 +921,17 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
         S.phi = p->d_phi;
     }
+    if (p->strategy == CVQ_STRATEGY_SORTED) {          // reachable nodes sorted by their exact threshold v*
+        std::vector<uint32_t> idx;
+        build_sorted_nodes(p->hx, S, kmax, p->hvs, idx);
+        if ((rc = dev_alloc(&p->d_sidx, idx.size())) || (rc = dev_alloc(&p->d_svs, idx.size()))) {
+            cvq_plan_destroy(p);
+            return rc;
+        }
+        e = hipMemcpy(p->d_sidx, idx.data(), idx.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_svs, p->hvs.data(), idx.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
+    }
     if (p->strategy == CVQ_STRATEGY_COMPACT) {         // exact level thresholds + grid lookup buckets
         std::vector<double> vs;
         build_vstar(p->hx, S.w0, S.w1, vs);
@@ -817,7 +959,8 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_vstar, (void*)p->d_bucket})
+                    (void*)p->d_cutfix, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_tree})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
@@ -919,7 +1062,7 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
 int32_t cvq_slab(cvq_plan* p, const double* bounds, double* out, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && bounds != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
-    if (mem != CVQ_MEM_DEVICE && p->strategy == CVQ_STRATEGY_PREFIX) {
+    if (mem != CVQ_MEM_DEVICE && materialised(p)) {
         for (long long t = 0; t < 2 * p->T; ++t)
             CVQ_REQUIRE(!(bounds[t] > p->v_cap), CVQ_ERR_RANGE, "a bound exceeds the plan's v_cap");
     }

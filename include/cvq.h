@@ -44,10 +44,12 @@ extern "C" {
 #define CVQ_GARCH 1
 #define CVQ_UKF   2
 
-/* quadrature strategy (both reproduce the reference) */
+/* quadrature strategy (all reproduce the reference) */
 #define CVQ_STRATEGY_PREFIX 0    /* materialise per-date row-prefix joint mass, then solve */
 #define CVQ_STRATEGY_DIRECT 1    /* evaluate each slab's nodes inside the solve kernel     */
 #define CVQ_STRATEGY_COMPACT 2   /* DIRECT control flow, one barrier per level, one-wave tail */
+#define CVQ_STRATEGY_SORTED 3    /* reachable nodes sorted by membership threshold: a slab is
+                                    one contiguous range (2-D, and 3-D with n <= 255)       */
 
 typedef struct cvq_plan cvq_plan;
 

@@ -70,7 +70,7 @@ def test_special_functions_vs_scipy_and_mpmath():
     assert np.max(np.abs(got - k["erf"])) <= 2.3e-16
 
 
-STRATEGIES = ["prefix", "direct", "compact"]
+STRATEGIES = ["prefix", "direct", "compact", "sorted"]
 
 
 def _skip_unsupported(z, strategy):
