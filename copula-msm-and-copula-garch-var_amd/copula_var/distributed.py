@@ -51,45 +51,55 @@ class ShardedVaR:
     local(hdr, snaps): solve this rank's block; hdr is int64[2] (the 16-byte
         cvq Header), snaps float64[per, stride] (rows past the block stay NaN).
     finalize(hdr_all, snaps_all, var): full VaR vector from the gathered data.
+    check(): optional convergence check after the finalize (raises on failure).
     """
 
     def __init__(self, T_total: int, stride: int, local: Callable, finalize: Callable,
-                 device: torch.device, group=None):
+                 device: torch.device, group=None, check: Optional[Callable] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.T_total = int(T_total)
         self.lo, self.hi, self.per = shard(self.T_total, self.rank, self.world)
         self.stride = int(stride)
-        self._local, self._finalize = local, finalize
+        self._local, self._finalize, self._check = local, finalize, check
         self.hdr = torch.zeros(2, dtype=torch.int64, device=device)
         self.snaps = torch.full((self.per, self.stride), float("nan"), dtype=torch.float64, device=device)
         self.var = torch.empty(self.T_total, dtype=torch.float64, device=device)
 
-    def solve(self) -> torch.Tensor:
+    def solve(self, check: bool = True) -> torch.Tensor:
+        """Full VaR vector on every rank.  check: verify convergence within the
+        bisection budget after the finalize (synchronises; the status is global, from
+        the gathered headers, so every rank raises together)."""
         self._local(self.hdr, self.snaps)
         if self.world == 1:
             self._finalize(self.hdr, self.snaps, self.var)
-            return self.var
-        hdr_all = _gather(self.hdr, self.world, self.group)
-        snaps_all = _gather(self.snaps, self.world, self.group)
-        self._finalize(hdr_all, snaps_all, self.var)
+        else:
+            hdr_all = _gather(self.hdr, self.world, self.group)
+            snaps_all = _gather(self.snaps, self.world, self.group)
+            self._finalize(hdr_all, snaps_all, self.var)
+        if check and self._check is not None:
+            self._check()
         return self.var
 
 
 def device_sharded_var(plan, args, T_total: int, device: torch.device, group=None) -> ShardedVaR:
-    """ShardedVaR wired to a QuadraturePlan's device entry points (plan holds this rank's block)."""
+    """ShardedVaR wired to a QuadraturePlan's device entry points (plan holds this rank's block).
+
+    The plan is bound to torch's current stream at every solve, so its kernels, the
+    snapshot buffers' initialisation and the collectives are ordered on one stream."""
     stride = plan.snap_stride(args)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     holder: dict = {}
 
     def local(hdr, snaps):
+        plan.set_stream(torch.cuda.current_stream(device).cuda_stream)
         plan.solve_local(args, hdr.data_ptr(), snaps.data_ptr())
 
     def finalize(hdr_all, snaps_all, var):
         plan.solve_finalize(args, hdr_all.data_ptr(), world, snaps_all.data_ptr(), holder["per"], T_total,
                             var.data_ptr())
 
-    s = ShardedVaR(T_total, stride, local, finalize, device, group)
+    s = ShardedVaR(T_total, stride, local, finalize, device, group, check=plan.solve_status)
     holder["per"] = s.per
     return s

@@ -155,9 +155,26 @@ class QuadraturePlan:
         return out, int(it.value)
 
     # ------------------------------------------------------------ device-resident solve
-    def solve_device(self, args: N.CvqSolveArgs, var_ptr: int) -> None:
-        """calc_var into a device buffer, in stream order, no host synchronisation."""
-        N.check(N.lib().cvq_solve(self._h, C.byref(args), C.c_void_p(var_ptr), None, N.MEM_DEVICE), "cvq_solve")
+    def solve_device(self, args: N.CvqSolveArgs, var_ptr: int, check: bool = False) -> Optional[int]:
+        """calc_var into a device buffer.  check=False: in stream order, no host
+        synchronisation and no convergence check (call solve_status() to check);
+        check=True: synchronises, widens the bisection budget if a date needed more
+        iterations (non-dyadic guesses) and returns the iteration count."""
+        if not check:
+            N.check(N.lib().cvq_solve(self._h, C.byref(args), C.c_void_p(var_ptr), None, N.MEM_DEVICE), "cvq_solve")
+            return None
+        it = C.c_int32(0)
+        N.check(N.lib().cvq_solve(self._h, C.byref(args), C.c_void_p(var_ptr), C.byref(it), N.MEM_DEVICE),
+                "cvq_solve")
+        return int(it.value)
+
+    def solve_status(self) -> int:
+        """Synchronise and check the last device-mode solve / finalize: raises NativeError
+        (CVQ_ERR_NUMERIC) if a date did not converge within the bisection budget; returns
+        the reference's bisection iteration count."""
+        it = C.c_int32(0)
+        N.check(N.lib().cvq_solve_status(self._h, C.byref(it)), "cvq_solve_status")
+        return int(it.value)
 
     @staticmethod
     def snap_stride(args: N.CvqSolveArgs) -> int:

@@ -7,16 +7,20 @@ second_guess) -> np.ndarray (T,)`` and ``compute_integral(bounds) -> (T,)``
 
 * ``compute_integral`` is one device slab launch (cvq_slab) instead of
   np.unique + nested-grid build + joblib over dates (calc_var_class.py:179-212);
-* ``calc_var`` is one device solve (cvq_solve: k_tables -> k_direct ->
-  k_finalize) that reproduces calc_var + bisection_algorithm (:95-177,
-  :250-309) with quirks Q1-Q4 -- results bit-identical to the reference on the
-  golden cases (tests/test_gpu_parity.py, tests/test_driver_gpu.py);
+* ``calc_var`` is one device solve (cvq_solve: one k_compact launch for 2 assets,
+  one k_sorted launch for 3, each with the finalize fused in) that reproduces
+  calc_var + bisection_algorithm (:95-177, :250-309) with quirks Q1-Q4 -- results
+  bit-identical to the reference on the golden cases (tests/test_gpu_parity.py,
+  tests/test_driver_gpu.py);
 * ``bisection_algorithm`` / ``adjust_integral`` keep the reference's host loop
   over device slabs, for callers that drive the bisection themselves.
 
-Keyword-only additions: ``copula_params`` (inject the packed copula parameters;
-the in-sample copula fit is out of scope), ``device``, ``strategy``
-("auto" = DIRECT for 2 assets, PREFIX for 3).
+The in-sample stage runs as the reference's does (model fits, marginals, the IFM
+copula fit of calc_copula_params, :77-82) on the device likelihoods.
+
+Keyword-only additions: ``copula_params`` (packed copula parameters that override
+the IFM fit), ``device``, ``strategy`` ("auto" = COMPACT for 2 assets, SORTED for
+3; or "direct", "prefix", "sorted", "compact").
 """
 from __future__ import annotations
 
@@ -57,8 +61,6 @@ class ValueAtRiskCalcualtion:
         self.unpack_copula_params = VaRCalculationMethod.unpack_copula_params
         self.integrated_function = VaRCalculationMethod.integrated_function
 
-        if strategy == "auto":
-            strategy = "compact" if self.dim == 2 else "prefix"
         densities, x_values, step_size, combos = self.grids_generations_params
         self.plan = QuadraturePlan(VaRCalculationMethod.model_kind, VaRCalculationMethod.copula_kind, self.dim,
                                    x_values, step_size, densities, combos, self.weights, self.copula_params,

@@ -1114,6 +1114,19 @@ int32_t cvq_solve_finalize(cvq_plan* p, const cvq_solve_args* a, const void* d_h
     return CVQ_OK;
 }
 
+int32_t cvq_solve_status(cvq_plan* p, int32_t* iters_out) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));
+    int err[3] = {0, 0, 0};
+    CVQ_HIP_CHECK(hipMemcpyAsync(err, p->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    if (iters_out) *iters_out = err[1];
+    CVQ_REQUIRE(err[0] == 0, CVQ_ERR_NUMERIC,
+                (err[0] & 2) ? "bisection needs more iterations than the snapshot budget (K)"
+                             : "a date did not converge within the bisection budget (K)");
+    return CVQ_OK;
+}
+
 int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t* iters_out, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);

@@ -136,6 +136,15 @@ int32_t cvq_slab(cvq_plan* plan, const double* bounds, double* out, int32_t mem)
 int32_t cvq_solve(cvq_plan* plan, const cvq_solve_args* args, double* var_out,
                   int32_t* iters_out, int32_t mem);
 
+/* Status of the plan's last device-mode solve or finalize (cvq_solve with
+ * CVQ_MEM_DEVICE and iters_out == NULL, cvq_solve_finalize): synchronises the
+ * plan's stream and returns CVQ_ERR_NUMERIC if a date did not converge within the
+ * bisection budget K (only possible for non-dyadic guesses, whose K carries a
+ * 2-iteration margin); iters_out = bisection iterations the reference runs (Q2/Q4).
+ * Device mode never synchronises by itself: call this to check.  cvq_solve with a
+ * non-NULL iters_out checks and widens K itself. */
+int32_t cvq_solve_status(cvq_plan* plan, int32_t* iters_out);
+
 /* Sharded solve, for one process per GPU (date blocks).
  * Phase 1 (local):  per-date bisection snapshots + a 16-byte header
  *   d_header: 16 bytes device, d_snaps: [T_local][cvq_snap_stride(args)] device.

@@ -12,8 +12,11 @@ path (tests/golden/_shims), and writes inputs + the reference's outputs:
   at a set of parameter rows per (p, q).
 * optim_msm_ll.npz -- ProbEstimation(k, m0, sigma, b, gamma, returns).calc_likelihood()
   (markov_switching_multifractal/calc_prob.py) at a set of parameter rows.
+* optim_msm_marg.npz -- calc_marginals / calc_densities
+  (markov_switching_multifractal/calc_marginals.py:7-30, the in-sample MSM marginals
+  and densities of msm_estimation.py:55-120) on the same returns and parameter rows.
 
-Usage:  python tests/golden/gen_optim_golden.py
+Usage:  python tests/golden/gen_optim_golden.py [all|msm_marginals]
 """
 from __future__ import annotations
 
@@ -95,5 +98,27 @@ def main():
     print("msm ll:", vals)
 
 
+def msm_marginals():
+    import matplotlib
+    matplotlib.use("Agg")
+    from markov_switching_multifractal.calc_marginals import calc_densities, calc_marginals
+    z = np.load(os.path.join(HERE, "optim_msm_ll.npz"))
+    x, k = z["returns"], int(z["k"])
+    marg, eps, dens, vol = [], [], [], []
+    for m0, sig, b, g in z["rows"]:
+        m, e, v = calc_marginals(k, m0, sig, b, g, x)
+        marg.append(m)
+        eps.append(e)
+        vol.append(v)
+        dens.append(calc_densities(k, m0, sig, b, g, x))
+    np.savez(os.path.join(HERE, "optim_msm_marg.npz"), returns=x, k=k, rows=z["rows"], marginals=np.array(marg),
+             eps=np.array(eps), densities=np.array(dens), vol_states=np.array(vol))
+    print("msm marginals:", np.array(marg).shape, np.array(dens).shape)
+
+
 if __name__ == "__main__":
-    main()
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("all", "optim"):
+        main()
+    if what in ("all", "msm_marginals"):
+        msm_marginals()

@@ -30,6 +30,19 @@ def test_msm_marginals_shapes_and_ranges():
     assert np.all((m > 0) & (m < 1)) and np.all(d > 0)
 
 
+def test_msm_marginals_match_reference():
+    """calc_marginals / calc_densities (calc_marginals.py:7-30) run by the reference itself
+    (optim_msm_marg.npz).  The filter's A @ prev (BLAS) sums in another order than the
+    reference's per-row loop (calc_prob.py:56-57), so the bar is relative, not bitwise."""
+    from copula_var.insample import msm_marginals_densities
+    z = load_golden("optim_msm_marg")
+    for row, mw, dw, vw in zip(z["rows"], z["marginals"], z["densities"], z["vol_states"]):
+        m, d, vol = msm_marginals_densities(z["returns"], int(z["k"]), *row)
+        np.testing.assert_array_equal(vol, vw)
+        np.testing.assert_allclose(m, mw, rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(d, dw, rtol=1e-12, atol=1e-300)
+
+
 @pytest.mark.parametrize("p,q", [(1, 1), (2, 1), (2, 2)])
 def test_garch_eps_reproduces_reference_variances(p, q):
     from copula_var.insample import garch_eps, garch_marginals_densities

@@ -66,3 +66,60 @@ def test_sharded_device_solve(case, ranks, strategy):
     finally:
         for p in plans:
             p.close()
+
+
+@pytest.mark.parametrize("strategy", ["compact", "sorted"])
+def test_device_sharded_var_orders_on_torch_stream(strategy):
+    """device_sharded_var binds the plan to torch's current stream itself (no explicit
+    set_stream): the snapshot buffer's NaN fill, the solve and the finalize are ordered."""
+    from copula_var import engine
+    from copula_var.distributed import device_sharded_var
+    from copula_var.engine import QuadraturePlan
+    z = load_golden("cfg2_n256")
+    p = QuadraturePlan(str(z["model"]), str(z["copula"]), 2, z["x_values"], z["step"], z["densities"],
+                       z["combos"], z["weights"], z["copula_params"], vol_states=z["unique_vol_states"],
+                       strategy=strategy)
+    try:
+        p.set_dates((z["forecasts_by_states"], z["forecasts"]))
+        args = engine.solve_args(float(z["ptf_mean"]))
+        s = device_sharded_var(p, args, z["var"].size, torch.device("cuda", 0))
+        for _ in range(3):
+            got = s.solve().cpu().numpy()
+            assert np.array_equal(got, z["var"])
+        assert p.solve_status() == int(z["n_calls"]) - 2
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("strategy", ["compact", "direct", "prefix", "sorted"])
+def test_non_dyadic_guesses_device_mode(strategy):
+    """Non-dyadic guesses (K carries a margin): solve_device(check=True), the sharded
+    path and the host path all agree with the oracle; solve_status reports the count."""
+    from copula_var import engine
+    from copula_var.distributed import device_sharded_var
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden("cfg2_n64")
+    kw = dict(first_guess=-2.7, second_guess=(-3.3, -2.1))
+    per = (z["forecasts_by_states"], z["forecasts"])
+    cargs = (str(z["model"]), str(z["copula"]), 2, z["x_values"], z["step"], z["densities"], z["combos"],
+             z["weights"], z["copula_params"])
+    P = Problem(*cargs, per, z["unique_vol_states"])
+    ref, ref_it, _ = calc_var(P.compute_integral, P.T, float(z["ptf_mean"]), **kw)
+    p = QuadraturePlan(*cargs, vol_states=z["unique_vol_states"], strategy=strategy)
+    try:
+        p.set_dates(per)
+        host, it = p.calc_var(float(z["ptf_mean"]), **kw)
+        assert it == ref_it and np.array_equal(host, ref)
+        args = engine.solve_args(float(z["ptf_mean"]), **kw)
+        p.set_stream(torch.cuda.current_stream().cuda_stream)
+        var = torch.empty(P.T, dtype=torch.float64, device="cuda")
+        assert p.solve_device(args, var.data_ptr(), check=True) == ref_it
+        assert np.array_equal(var.cpu().numpy(), ref)
+        p.solve_device(args, var.data_ptr())
+        assert p.solve_status() == ref_it
+        assert np.array_equal(var.cpu().numpy(), ref)
+        s = device_sharded_var(p, args, P.T, torch.device("cuda", 0))
+        assert np.array_equal(s.solve().cpu().numpy(), ref)
+    finally:
+        p.close()
