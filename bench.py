@@ -51,9 +51,10 @@ def parse():
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
     ap.add_argument("--strategy", default="auto", choices=["auto", "prefix", "direct", "compact", "sorted"],
-                    help="auto: COMPACT for 2 assets, SORTED for 3")
+                    help="auto: COMPACT for 2-asset MSM, SORTED otherwise (engine.auto_strategy)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
-    ap.add_argument("--cpu-dates", type=int, default=0, help="CPU sample size (0 = one per worker)")
+    ap.add_argument("--cpu-dates", type=int, default=0,
+                    help="CPU sample size (0 = four per worker: ~15 s of joblib work on config 2)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=0, help="also time the device forecast stage")
     ap.add_argument("--inflight", type=int, default=2,
@@ -96,7 +97,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = synthetic.baseline_configs()[a.config]
     if a.strategy == "auto":
-        a.strategy = "compact" if cfg.dim == 2 else "sorted"
+        a.strategy = engine.auto_strategy(cfg.model, cfg.dim)
     per_gpu = a.dates_per_gpu or cfg.T
     T_total = per_gpu * world
     c, ipt, uvs, ggp, ptf_mean, per, t_fc, block = build_inputs(cfg, T_total, rank, world, local)
@@ -242,7 +243,7 @@ def cpu_baseline(c, ipt, uvs, ggp, ptf_mean, gpu_var, a):
     from oracle import quadrature as Q
     from oracle.joblib_port import JoblibPath
     jobs = a.cpu_jobs or min(16, os.cpu_count() or 1)
-    S = a.cpu_dates or jobs
+    S = a.cpu_dates or 4 * jobs
     dens, x, step, combos = ggp
     if c.model == "msm":
         per = (ipt[0][:S], ipt[1][:S])

@@ -29,6 +29,14 @@ def solve_args(ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_gue
                           float(min_var), float(max_var), float(lower), float(tolerance), float(ptf_mean))
 
 
+def auto_strategy(model: str, dim: int) -> str:
+    """The measured-fastest strategy per workload (cfg 1-5 on one MI355X):
+    COMPACT for 2-asset MSM (cfg 2: 17.5M vs SORTED 15.7M VaR-dates/s), SORTED for
+    2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for 3 assets (the only
+    strategy that runs the 128^3 grid of cfg 4)."""
+    return "compact" if (dim == 2 and model == "msm") else "sorted"
+
+
 class QuadraturePlan:
     """One device plan: static grid tables + copula + per-date inputs on one GPU."""
 
@@ -60,8 +68,8 @@ class QuadraturePlan:
         st.vol_states = dp(self._vs) if self._vs is not None else None
         st.copula_params = dp(self._cp)
         st.n_copula_params = self._cp.size
-        if strategy == "auto":                          # DIRECT / COMPACT are built for 2 assets
-            strategy = "compact" if self.dim == 2 else "sorted"
+        if strategy == "auto":
+            strategy = auto_strategy(model, self.dim)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
                        "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED}[strategy]
         self.strategy = strategy

@@ -19,8 +19,8 @@ The in-sample stage runs as the reference's does (model fits, marginals, the IFM
 copula fit of calc_copula_params, :77-82) on the device likelihoods.
 
 Keyword-only additions: ``copula_params`` (packed copula parameters that override
-the IFM fit), ``device``, ``strategy`` ("auto" = COMPACT for 2 assets, SORTED for
-3; or "direct", "prefix", "sorted", "compact").
+the IFM fit), ``device``, ``strategy`` ("auto" = COMPACT for 2-asset MSM, SORTED for
+3 assets and for 2-asset GARCH / UKF, engine.auto_strategy; or "direct", "prefix", "sorted", "compact").
 """
 from __future__ import annotations
 

@@ -394,7 +394,8 @@ void build_vstar(const std::vector<double>& x, double w0, double w1, std::vector
 }
 
 // SORTED: every reachable node (row r, inner j in [1, kmax_r]) with its v*, sorted
-// by (v*, packed index); packed = i0 | j << 16 (2-D), i0 | i1 << 8 | j << 16 (3-D).
+// by (v*, packed index); packed = i0 | j << 16 (2-D), a0 | i1 << 9 | j << 17 (3-D) with
+// a0 = i0 + n on the plane i1 == 0 (the Q6 plane has its own axis-0 records).
 void build_sorted_nodes(const std::vector<double>& x, const StaticDev& S, const std::vector<int>& kmax,
                         std::vector<double>& vs, std::vector<uint32_t>& idx) {
     const int n = S.n;
@@ -403,8 +404,9 @@ void build_sorted_nodes(const std::vector<double>& x, const StaticDev& S, const 
     for (int r = 0; r < S.nrows; ++r) {
         const int i0 = S.dim == 2 ? r : r / n, i1 = S.dim == 2 ? 0 : r % n;
         const double lev = S.dim == 2 ? x[i0] * S.w1 : x[i0] * S.w1 + x[i1] * S.w2;   // integration_algo.py:20
-        const uint32_t base = S.dim == 2 ? (uint32_t)i0 : (uint32_t)(i0 | (i1 << 8));
-        for (int j = 1; j <= kmax[r]; ++j) nodes.emplace_back(vstar_exact(x[j], lev, S.w0), base | ((uint32_t)j << 16));
+        const uint32_t base = S.dim == 2 ? (uint32_t)i0 : (uint32_t)((i0 + (i1 == 0 ? n : 0)) | (i1 << 9));
+        const int jsh = S.dim == 2 ? 16 : 17;
+        for (int j = 1; j <= kmax[r]; ++j) nodes.emplace_back(vstar_exact(x[j], lev, S.w0), base | ((uint32_t)j << jsh));
     }
     std::sort(nodes.begin(), nodes.end());
     vs.resize(nodes.size());
@@ -421,7 +423,7 @@ int host_ub(const std::vector<double>& vs, double v) {        // #{v* <= v}; NaN
 }
 
 // ub() of the fixed levels and, per bracket, of the bisection mids down to the depth
-// where every cell holds <= kSortTailCap nodes (the device searches deeper levels).
+// where every cell holds <= sorted_tail_cap(dim) nodes (the device searches deeper levels).
 int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
     const double key[7] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax, (double)P.K};
     if (p->tree_valid && std::memcmp(key, p->tree_key, sizeof key) == 0) return CVQ_OK;
@@ -445,7 +447,7 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
                     const double mid = (l + h) / 2;
                     if ((node >> bit) & 1) l = mid; else h = mid;
                 }
-                if (host_ub(vs, h) - host_ub(vs, l) > kSortTailCap) small = false;
+                if (host_ub(vs, h) - host_ub(vs, l) > sorted_tail_cap(p->S.dim)) small = false;
             }
         }
         if (small) { depth = d; break; }
@@ -517,7 +519,7 @@ int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G
                    double* snaps, Header* hdr);
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
-                  const double* bounds, double* out, double* snaps, Header* hdr);           // cvq_sorted.hip
+                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps);  // cvq_sorted.hip
 }
 namespace {
 
@@ -535,9 +537,13 @@ SortedGeom sorted_geom(const cvq_plan* p) {
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
     if (p->strategy == CVQ_STRATEGY_SORTED) {
-        if (int rc = ensure_sorted_tree(p, P)) return rc;
+        int rc = ensure_sorted_tree(p, P);
+        if (rc) return rc;
+        static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;   // diagnostic phase stamps
+        if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
-                             direct_fused(p), 0, nullptr, nullptr, snaps, hdr);
+                             direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
+                             dbg_stamps ? (double*)p->d_stamps : nullptr);
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
@@ -579,7 +585,7 @@ int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     if (p->strategy == CVQ_STRATEGY_SORTED) {
         SolveConst P{};
         return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
-                             direct_fused(p), 1, bounds, out, nullptr, nullptr);
+                             direct_fused(p), 1, bounds, out, nullptr, nullptr, nullptr);
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {      // COMPACT: slabs of arbitrary bounds run k_direct
         SolveConst P{};
@@ -1008,7 +1014,7 @@ int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_
 
 int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
     CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
-    CVQ_REQUIRE(p->d_stamps != nullptr, CVQ_ERR_STATE, "no stamps recorded (set CVQ_STAMPS=1, DIRECT strategy)");
+    CVQ_REQUIRE(p->d_stamps != nullptr, CVQ_ERR_STATE, "no stamps recorded (set CVQ_STAMPS=1; DIRECT, COMPACT or SORTED strategy)");
     CVQ_REQUIRE(count <= p->capStamps * 32, CVQ_ERR_INVALID, "count exceeds the stamp buffer");
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     CVQ_HIP_CHECK(hipMemcpy(host, p->d_stamps, count * 8, hipMemcpyDeviceToHost));

@@ -24,13 +24,14 @@ struct SortedLaunch {
     double *out, *snaps;
     Header* hdr;
     bool fused;
+    double* stamps;
 };
 
 template <int COP, bool MSM, int DIM, int PM, bool FUSED>
 void launch_f(const SortedLaunch& L) {
     hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED>), dim3((unsigned)L.T), dim3(kSortNT),
-                       sorted_lds_bytes(L.S.n, kSortNT), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode,
-                       L.bounds, L.out, L.snaps, L.hdr);
+                       sorted_lds_bytes(L.S.n, kSortNT, DIM), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode,
+                       L.bounds, L.out, L.snaps, L.hdr, L.stamps);
 }
 
 template <int COP, bool MSM, int DIM, int PM>
@@ -64,9 +65,9 @@ void launch_c(const SortedLaunch& L) {
 
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
-                  const double* bounds, double* out, double* snaps, Header* hdr) {
-    CVQ_REQUIRE(S.n <= (S.dim == 2 ? 65535 : 255), CVQ_ERR_UNSUPPORTED, "SORTED packs grid indices in 16 / 8 bits");
-    const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused};
+                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps) {
+    CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
+    const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps};
     switch (S.copula) {
         case CVQ_GAUSSIAN: launch_c<CVQ_GAUSSIAN>(L); break;
         case CVQ_STUDENT: launch_c<CVQ_STUDENT>(L); break;

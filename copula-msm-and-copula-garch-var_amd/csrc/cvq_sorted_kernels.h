@@ -14,7 +14,7 @@
 // (lower, first / second guesses, min / max VaR) and the bisection mids, which
 // form one binary tree per bracket ((lo + hi) / 2 from the bracket's ends).  The
 // host tabulates ub() of the fixed levels and of the tree's mids down to the
-// depth where every cell holds <= kSortTailCap nodes, so a level costs one
+// depth where every cell holds <= sorted_tail_cap nodes, so a level costs one
 // table read, the slab's node evaluations spread evenly over the workgroup, and
 // one reduction.  Beyond that depth the bracket's nodes go to LDS and one wave
 // finishes the remaining levels with masked wave sums (COMPACT's tail).
@@ -35,14 +35,23 @@
 
 namespace cvq {
 
-constexpr int kSortTailPerLane = 4;
-constexpr int kSortTailCap = 64 * kSortTailPerLane;   // bracket size that switches to the one-wave tail
+// Tail nodes per lane of the one-wave tail (bracket size that switches to it = 64x):
+// measured best 4 for 2-D (LDS-bound occupancy at n = 256), 16 for 3-D.
+#ifndef CVQ_SORT_TAIL2
+#define CVQ_SORT_TAIL2 4
+#endif
+#ifndef CVQ_SORT_TAIL3
+#define CVQ_SORT_TAIL3 16
+#endif
+__host__ __device__ constexpr int sorted_tail_per_lane(int dim) { return dim == 2 ? CVQ_SORT_TAIL2 : CVQ_SORT_TAIL3; }
+__host__ __device__ constexpr int sorted_tail_cap(int dim) { return 64 * sorted_tail_per_lane(dim); }
 constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisection level
 constexpr int kSortIlp = 4;                           // nodes in flight per thread
 
 // Date-independent device tables of a SORTED plan.
 struct SortedGeom {
-    const uint32_t* idx;   // [G] packed node indices, sorted by v* (2-D: i0 | j << 16; 3-D: i0 | i1 << 8 | i2 << 16)
+    const uint32_t* idx;   // [G] packed node indices, sorted by v* (2-D: i0 | j << 16;
+                           //     3-D: a0 | i1 << 9 | j << 17, a0 = i0 + n [i1 == 0], the Q6 plane)
     const double* vs;      // [G] the sorted v*
     const int* tree;       // [4][1 << depth]: ub(mid) of heap node h (1 <= h < 2^depth) of each bracket's tree
     int G;
@@ -50,26 +59,25 @@ struct SortedGeom {
     int fix[6];            // ub() of lower, sg0, fg, sg1, vmin, vmax
 };
 
-// exp(x): 2^k e^r, |r| <= ln2 / 2, degree-11 Taylor polynomial (relative error
-// ~1e-15; the solve's decisions are unchanged by 1e-8 node noise).
-// x < -800 underflows to 0, NaN stays NaN.
+// exp(x): 2^k e^r, |r| <= ln2 / 2, degree-9 polynomial fitted to exp's relative
+// error on that interval (max 1.4e-14; the solve's decisions are unchanged by 1e-8
+// node noise).  For finite |x| < 1e9 (the fast records clamp their
+// logs at kLogFloor); x < -1075 underflows to 0, NaN stays NaN.
+constexpr double kLogFloor = -1.0e4;
 __device__ __forceinline__ double exp_node(double x) {
-    x = x < -800.0 ? -800.0 : x;
     const double k = __builtin_rint(x * 1.4426950408889634);
     double r = fma(-k, 6.93147180369123816490e-01, x);      // ln2 hi (exact k * hi for |k| < 2^20)
     r = fma(-k, 1.90821492927058770002e-10, r);             // ln2 lo
-    double p = 2.505210838544172e-08;                        // 1 / 11!
-    p = fma(p, r, 2.755731922398589e-07);
-    p = fma(p, r, 2.7557319223985893e-06);
-    p = fma(p, r, 2.48015873015873e-05);
-    p = fma(p, r, 0.0001984126984126984);
-    p = fma(p, r, 0.001388888888888889);
-    p = fma(p, r, 0.008333333333333333);
-    p = fma(p, r, 0.041666666666666664);
-    p = fma(p, r, 0.16666666666666666);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
+    double p = 2.747468209548047e-06;
+    p = fma(p, r, 2.488396512173419e-05);
+    p = fma(p, r, 0.00019841616545137992);
+    p = fma(p, r, 0.001388880293639777);
+    p = fma(p, r, 0.008333332984833044);
+    p = fma(p, r, 0.041666667031658604);
+    p = fma(p, r, 0.1666666666788623);
+    p = fma(p, r, 0.499999999994599);
+    p = fma(p, r, 0.9999999999998875);
+    p = fma(p, r, 1.0000000000000127);
     return __builtin_amdgcn_ldexp(p, (int)k);
 }
 
@@ -83,61 +91,93 @@ __device__ __forceinline__ int sorted_ub(const double* __restrict__ vs, int lo, 
     return lo;
 }
 
+// a0: axis-0 record index (3-D: i0 + n on the plane i1 == 0), i1, j
 template <int DIM>
-__device__ __forceinline__ void unpack_node(uint32_t c, int* i0, int* i1, int* j) {
+__device__ __forceinline__ void unpack_node(uint32_t c, int* a0, int* i1, int* j) {
     if constexpr (DIM == 2) {
-        *i0 = (int)(c & 0xFFFFu);
+        *a0 = (int)(c & 0xFFFFu);
         *i1 = 0;
         *j = (int)(c >> 16);
     } else {
-        *i0 = (int)(c & 0xFFu);
-        *i1 = (int)((c >> 8) & 0xFFu);
-        *j = (int)(c >> 16);
+        *a0 = (int)__builtin_amdgcn_ubfe(c, 0, 9);
+        *i1 = (int)__builtin_amdgcn_ubfe(c, 9, 8);
+        *j = (int)(c >> 17);
     }
 }
 
-// LDS doubles per grid point: generic z / B / w of 3 axes (9), fast records (8);
-// arrays are laid out with an even stride so every double2 is 16-B aligned.
-constexpr int kSortLdsPerPoint = 17;
+// LDS doubles per grid point of the table region: the generic tables (3 DIM) or the
+// fast records (16-B records per axis entry, 3-D: axis 0 twice + one extra axis-1
+// value), whichever is larger; arrays are laid out with an even stride so every
+// double2 is 16-B aligned.  16-B records keep a node at 32 B of LDS reads (2-D):
+// the node loop is LDS-bandwidth bound, so wider records cost more than the VALU
+// work they save (measured).
+// largest n the kernel's register tables hold: the plan's 512 in 2-D, the 8-bit packing's 255 in 3-D
+__host__ __device__ constexpr int sorted_max_n(int dim) { return dim == 2 ? 512 : 255; }
+__host__ __device__ constexpr int sorted_region(int dim) { return dim == 2 ? 6 : 9; }
 inline int sorted_stride(int n) { return (n + 1) & ~1; }
-inline size_t sorted_lds_bytes(int n, int nt) {
-    return sizeof(double) * (size_t)kSortLdsPerPoint * sorted_stride(n) + sizeof(double2) * kSortTailCap +
-           sizeof(double) * 6 * (nt / 64);
+inline size_t sorted_lds_bytes(int n, int nt, int dim) {
+    return sizeof(double) * (size_t)sorted_region(dim) * sorted_stride(n) + sizeof(double2) * sorted_tail_cap(dim) +
+           sizeof(double) * 2 * (nt / 64);
 }
 
 // mode 0: calc_var solve (snapshots + header, fused finalize when P.fin_var);
 // mode 1: one slab per date (compute_integral): out[t] = I_t(bounds[2t], bounds[2t+1]].
+// Minimum waves per SIMD asked of the register allocator: 5 for 2-D (measured
+// +15% on config 5, neutral on 2), none for 3-D (its exp chain needs the registers).
+#ifndef CVQ_SORT_MIN_WAVES2
+#define CVQ_SORT_MIN_WAVES2 5
+#endif
+__host__ __device__ constexpr int sorted_min_waves(int dim) { return dim == 2 ? CVQ_SORT_MIN_WAVES2 : 1; }
+
 template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED>
-__global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
+__global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
                                                const double* __restrict__ bounds, double* __restrict__ out,
-                                               double* __restrict__ snaps, Header* hdr) {
+                                               double* __restrict__ snaps, Header* hdr, double* __restrict__ stamps_out) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int TPL = sorted_tail_per_lane(DIM), TCAP = sorted_tail_cap(DIM);
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
     const int ns = (n + 1) & ~1;                   // sorted_stride(n)
     const long long t = blockIdx.x;
-    // generic tables (reference semantics): z, B, w per axis (axis 0 of 3-D: w = the i1 == 0 weight)
-    double* zg = lds;                              // [3][ns] (row ax at zg + ax * n, n <= ns)
-    double* Bg = zg + 3 * ns;                      // [3][ns]
-    double* wg = Bg + 3 * ns;                      // [3][ns]
-    double* fr0 = wg + 3 * ns;                     // [ns][2] fast axis 0
-    double* fd0 = fr0 + 2 * ns;                    // [ns]    fast axis 0, plane i1 == 0 (3-D)
-    double* fr1 = fd0 + ns;                        // [ns][2] fast axis 1 (3-D)
-    double* fg1 = fr1 + 2 * ns;                    // [ns]    fast axis 1, third value (3-D)
-    double* fr2 = fg1 + ns;                        // [ns][2] fast inner axis
-    double2* tail = (double2*)(fr2 + 2 * ns);      // [kSortTailCap] (v*, value)
-    double* red = (double*)(tail + kSortTailCap);  // [2][3][NT / 64]
-    __shared__ int flags;                          // bit 0: non-finite table entry, bit 1: pi not rank 1
+    // One LDS region holds EITHER the generic tables (reference semantics: z, B, w per
+    // axis; axis 0 of 3-D: w = the i1 == 0 weight) OR the fast records (16 B per axis
+    // entry; 3-D axis 0 twice, [n, 2n) = the plane i1 == 0), chosen per date.
+    double* zg = lds;                              // generic [DIM][n]
+    double* Bg = zg + DIM * ns;                    // generic [DIM][n]
+    double* wg = Bg + DIM * ns;                    // generic [DIM][n]
+    double* fr0 = lds;                             // fast [ns (3-D: 2 ns)][2] axis 0
+    double* fr1 = fr0 + (DIM == 3 ? 4 : 2) * ns;   // fast [ns][2] axis 1 (3-D)
+    double* fg1 = fr1 + (DIM == 3 ? 2 : 0) * ns;   // fast [ns] axis 1, third value (3-D)
+    double* fr2 = fg1 + (DIM == 3 ? 1 : 0) * ns;   // fast [ns][2] inner axis
+    double2* tail = (double2*)(lds + sorted_region(DIM) * ns);   // [TCAP] (v*, value)
+    double* red = (double*)(tail + TCAP);          // [2][NT / 64] reduction slots
+    __shared__ int flags;                          // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
     __shared__ double s_arest;                     // 3-D: the axis-0 weight off the plane i1 == 0
 
+    // diagnostic phase stamps (CVQ_STAMPS=1, never in a timed run): COMPACT's slots --
+    // 0 start, 1 tables, 2 first slab, 3 second slab, 4 bracket, 5 + level, 29 tail
+    // build, 31 end, 25 / 26 realtime; 28 = nodes this date evaluated
+    unsigned long long* stamps = stamps_out ? (unsigned long long*)stamps_out + t * 32 : nullptr;
+    auto stamp = [&](int idx) {
+        if (stamps && tid == 0 && idx < 32) stamps[idx] = __builtin_amdgcn_s_memtime();
+    };
+    long long nodes = 0;                           // nodes evaluated (thread 0, stamps only)
+    stamp(0);
+    if (stamps && tid == 0) stamps[25] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) flags = 0;
     __syncthreads();
-    // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi)
+    // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
+    // axes unrolled so their latencies overlap; kept in registers until the path is chosen
+    constexpr int RPT = (sorted_max_n(DIM) + NT - 1) / NT;       // grid indices per thread
     const int q = MSM ? S.q : 1;
     const double* fb = MSM ? a + t * DIM * q : nullptr;     // forecasts_by_states[t] (DIM, q)
+    double eA[RPT][DIM], eB[RPT][DIM], eW[RPT][DIM];
     int bad = 0;
-    for (int i = tid; i < n; i += NT) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int i = tid + k * NT;
+        if (i >= n) continue;
 #pragma unroll
         for (int ax = 0; ax < DIM; ++ax) {
             double A, B;
@@ -152,14 +192,15 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
             double w;
             if constexpr (MSM) {
                 w = 0.0;
-                for (int s = 0; s < q; ++s) w = fma(fb[fax * q + s], S.F[((size_t)ax * q + s) * n + i], w);
+                for (int s2 = 0; s2 < q; ++s2) w = fma(fb[fax * q + s2], S.F[((size_t)ax * q + s2) * n + i], w);
             } else {
                 w = S.F[(size_t)ax * n + i];
             }
             if (!isfinite(A) || !isfinite(B)) bad |= 1;
-            zg[ax * n + i] = A;
-            Bg[ax * n + i] = B;
-            wg[ax * n + i] = w;
+            if (!(B * w > 0.0)) bad |= 1;                  // fast records take logs of B w
+            eA[k][ax] = A;
+            eB[k][ax] = B;
+            eW[k][ax] = w;
         }
     }
     const double* pit = pi + t * S.Q;
@@ -172,92 +213,117 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
         }
     }
     if (DIM == 3 && tid == 0) {                            // sum over L0 of pi's axis-0 factor off the plane
-        double s = 1.0;
+        double s0 = 1.0;
         if constexpr (MSM) {
-            s = 0.0;
-            for (int L = 0; L < q; ++L) s += fb[2 * q + L];
+            s0 = 0.0;
+            for (int L = 0; L < q; ++L) s0 += fb[2 * q + L];
         }
-        s_arest = s;
+        s_arest = s0;
     }
     if (bad) atomicOr(&flags, bad);
     __syncthreads();
     const int fl = flags;
     const bool rank1 = !(fl & 2);
-    const bool fast = rank1 && !(fl & 1) && COP != CVQ_PLACKETT;
+    const bool fast = rank1 && !(fl & 1);
     const double arest = DIM == 3 ? s_arest : 1.0;
-    if (fast) {                                            // fast records from the generic tables
-        for (int i = tid; i < n; i += NT) {
-            const double z0 = zg[i], zi = zg[(DIM - 1) * n + i];
-            const double B0 = Bg[i], Bi = Bg[(DIM - 1) * n + i];
-            const double w0 = wg[i], wi = wg[(DIM - 1) * n + i];
-            if constexpr (COP == CVQ_GAUSSIAN) {
-                const double s0 = DIM == 3 ? arest : w0;
-                fr0[2 * i] = DIM == 2 ? -(S.Ri[1] + S.Ri[2]) * 0.5 * z0 : z0;
-                fr0[2 * i + 1] = log(S.term1 * B0 * s0) - 0.5 * S.Ri[0] * (z0 * z0);
-                fr2[2 * i] = zi;
-                fr2[2 * i + 1] = log(Bi * wi) - 0.5 * S.Ri[DIM * DIM - 1] * (zi * zi);
-                if constexpr (DIM == 3) {
-                    const double z1 = zg[n + i];
-                    fd0[i] = log(w0) - log(arest);
-                    fr1[2 * i] = -(S.Ri[1] + S.Ri[3]) * 0.5 * z1;                    // c01 z1
-                    fr1[2 * i + 1] = -(S.Ri[5] + S.Ri[7]) * 0.5 * z1;                // c12 z1
-                    fg1[i] = log(Bg[n + i] * wg[n + i]) - 0.5 * S.Ri[4] * (z1 * z1);
+    // Gaussian: -z^T R^-1 z / 2 = sum_c -Ri_cc z_c^2 / 2 + c01 z0 z1 + c02 z0 z2 + c12 z1 z2;
+    // Student: 1 + z^T R^-1 z / nu = 1 + sum_c a_cc z_c^2 + a01 z0 z1 + a02 z0 z2 + a12 z1 z2
+    const double kq = COP == CVQ_GAUSSIAN ? -0.5 : S.inv_nu;
+    const double k01 = kq * (S.Ri[1] + S.Ri[DIM]);
+    const double k02 = DIM == 2 ? k01 : kq * (S.Ri[2] + S.Ri[6]);
+    const double k12 = DIM == 3 ? kq * (S.Ri[5] + S.Ri[7]) : 0.0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int i = tid + k * NT;
+      if (i >= n) continue;
+#pragma unroll
+      for (int ax = 0; ax < DIM; ++ax) {
+        const double z = eA[k][ax], B = eB[k][ax], w = eW[k][ax];
+        if (!fast) {
+            zg[ax * n + i] = z;
+            Bg[ax * n + i] = B;
+            wg[ax * n + i] = w;
+            continue;
+        }
+        const double kcc = kq * S.Ri[ax * (DIM + 1)] * (z * z);          // diagonal term of axis ax
+        if constexpr (COP == CVQ_GAUSSIAN) {
+            // log factors g = log(B w) - Ri_cc z^2 / 2, clamped at kLogFloor; E = sum g + cross
+            auto lg = [](double v) { return fmax(log(v), kLogFloor); };
+            if (ax == 0) {
+                fr0[2 * i] = DIM == 2 ? k02 * z : z;
+                fr0[2 * i + 1] = lg(S.term1 * B * (DIM == 3 ? arest : w)) + kcc;
+                if (DIM == 3) {                                              // plane i1 == 0 (Q6)
+                    fr0[2 * (n + i)] = z;
+                    fr0[2 * (n + i) + 1] = lg(S.term1 * B * w) + kcc;
                 }
-            } else {                                       // Student
-                const double s0 = DIM == 3 ? arest : w0;
-                fr0[2 * i] = z0;
-                fr0[2 * i + 1] = S.term1 * B0 * s0;
-                fr2[2 * i] = zi;
-                fr2[2 * i + 1] = Bi * wi;
-                if constexpr (DIM == 3) {
-                    fd0[i] = w0 / arest;
-                    fr1[2 * i] = zg[n + i];
-                    fr1[2 * i + 1] = Bg[n + i] * wg[n + i];
-                }
+            } else if (ax == DIM - 1) {
+                fr2[2 * i] = z;
+                fr2[2 * i + 1] = lg(B * w) + kcc;
+            } else {
+                fr1[2 * i] = k01 * z;
+                fr1[2 * i + 1] = k12 * z;
+                fg1[i] = lg(B * w) + kcc;
+            }
+        } else {                                           // Student: z and scale; Plackett: u and scale
+            const double sc = (ax == 0 && COP == CVQ_STUDENT ? S.term1 : 1.0) * B *
+                              (ax == 0 && DIM == 3 ? arest : w);
+            double* r = (ax == 0 ? fr0 : ax == DIM - 1 ? fr2 : fr1) + 2 * i;
+            r[0] = z;
+            r[1] = sc;
+            if (DIM == 3 && ax == 0) {                                       // plane i1 == 0 (Q6)
+                fr0[2 * (n + i)] = z;
+                fr0[2 * (n + i) + 1] = S.term1 * B * w;
             }
         }
+      }
     }
     __syncthreads();
 
-    // Gaussian cross coefficients (-z^T R^-1 z / 2), Student y = z^T R^-1 z / nu coefficients
-    const double c02 = -(S.Ri[2] + S.Ri[6]) * 0.5;
-    const double a00 = S.Ri[0] * S.inv_nu, a11 = S.Ri[DIM + 1] * S.inv_nu, a22 = S.Ri[DIM * DIM - 1] * S.inv_nu;
-    const double a01 = (S.Ri[1] + S.Ri[DIM]) * S.inv_nu;
-    const double a02 = DIM == 2 ? a01 : (S.Ri[2] + S.Ri[6]) * S.inv_nu;
-    const double a12 = DIM == 3 ? (S.Ri[5] + S.Ri[7]) * S.inv_nu : 0.0;
-
+    stamp(1);
+    // Student: b = 1 + z^T R^-1 z / nu = 1 + z0 (a00 z0 + k01 z1 + k02 z2) + z1 (a11 z1 + k12 z2) + a22 z2^2
+    const double a00 = kq * S.Ri[0], a11 = kq * S.Ri[DIM + 1], a22 = kq * S.Ri[DIM * DIM - 1];
     auto node_fast = [&](uint32_t c) -> double {
-        int i0, i1, j;
-        unpack_node<DIM>(c, &i0, &i1, &j);
-        const double2 A = *(const double2*)(fr0 + 2 * i0);
+        int a0, i1, j;
+        unpack_node<DIM>(c, &a0, &i1, &j);
+        const double2 A = *(const double2*)(fr0 + 2 * a0);
         const double2 C = *(const double2*)(fr2 + 2 * j);
         if constexpr (COP == CVQ_GAUSSIAN) {
             if constexpr (DIM == 2) {
                 return exp_node(fma(A.x, C.x, A.y + C.y));
             } else {
                 const double2 Bv = *(const double2*)(fr1 + 2 * i1);
-                double E = fma(A.x, fma(c02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + fg1[i1]) + C.y));
-                if (i1 == 0) E += fd0[i0];
-                return exp_node(E);
+                return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + fg1[i1]) + C.y)));
             }
-        } else {                                           // Student
-            double y, sc;
+        } else if constexpr (COP == CVQ_STUDENT) {
+            double b, sc;
             if constexpr (DIM == 2) {
-                y = fma(A.x, fma(a00, A.x, a02 * C.x), a22 * (C.x * C.x));
+                b = fma(A.x, fma(a00, A.x, k02 * C.x), fma(a22 * C.x, C.x, 1.0));
                 sc = A.y * C.y;
             } else {
                 const double2 Bv = *(const double2*)(fr1 + 2 * i1);
-                y = fma(A.x, fma(a00, A.x, fma(a01, Bv.x, a02 * C.x)), Bv.x * fma(a11, Bv.x, a12 * C.x));
-                y = fma(a22, C.x * C.x, y);
+                b = fma(A.x, fma(a00, A.x, fma(k01, Bv.x, k02 * C.x)), fma(Bv.x, fma(a11, Bv.x, k12 * C.x),
+                                                                              fma(a22 * C.x, C.x, 1.0)));
                 sc = (A.y * Bv.y) * C.y;
-                if (i1 == 0) sc *= fd0[i0];
             }
-            return sc * pow_node_t<PM>(1.0 + y, S.node_m, S.node_ex);
+            return sc * pow_node_t<PM>(b, S.node_m, S.node_ex);
+        } else {                                           // Plackett (plackett.py:66-69, Q11), 2-D
+            const double th = S.theta, a1 = th - 1.0, u = A.x, v = C.x, s2 = u + v;
+            const double num = th * fma(a1, fma(-2.0 * u, v, s2), 1.0);
+            const double d = fma(a1, s2, 1.0) * fma(-a1, s2, 1.0 + a1);
+            const double den = d * d;
+            double y = __builtin_amdgcn_rcp(den);
+            y = fma(y, fma(-den, y, 1.0), y);
+            y = fma(y, fma(-den, y, 1.0), y);
+            // num / 0 as IEEE division gives it (the Newton steps would give NaN)
+            const double c0 = den == 0.0 ? (num == 0.0 ? __builtin_nan("") : __builtin_copysign(__builtin_inf(), num))
+                                         : num * y;
+            return c0 * (A.y * C.y);
         }
     };
     auto node_generic = [&](uint32_t c) -> double {
         int i0, i1, j;
         unpack_node<DIM>(c, &i0, &i1, &j);
+        if (DIM == 3 && i0 >= n) i0 -= n;                  // the plane's axis-0 record index
         const double zi = zg[(DIM - 1) * n + j], Bi = Bg[(DIM - 1) * n + j];
         double W;
         if (rank1) {
@@ -288,7 +354,8 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
         else ctx = make_row<COP, 3>(S, zg[i0], zg[n + i1], Bg[i0] * Bg[n + i1]);
         return node_value<COP, MSM, DIM>(S, ctx, zi, Bi, W);
     };
-    // sum of the nodes at sorted positions [p0, p1), strided over the workgroup
+    // sum of the nodes at sorted positions [p0, p1), strided over the workgroup; the
+    // last (partial) round is predicated so its index loads are in flight together
     auto range_sum = [&](int p0, int p1) -> double {
         double acc[kSortIlp];
 #pragma unroll
@@ -302,17 +369,31 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
 #pragma unroll
                 for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(c[u]);
             }
-            for (; p < p1; p += NT) acc[0] += node_fast(G.idx[p]);
+            if (p < p1) {
+                uint32_t c[kSortIlp];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) c[u] = p + u * NT < p1 ? G.idx[p + u * NT] : 0u;
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u)
+                    if (p + u * NT < p1) acc[u] += node_fast(c[u]);
+            }
         } else {
             for (; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
         }
         return (acc[0] + acc[1]) + (acc[2] + acc[3]);
     };
     int parity = 0;
-    double sums[3];
-    auto team_sum = [&](double v) {
-        team_sum3<NT>(v, 0.0, 0.0, red, parity, sums);
-        return sums[0];
+    auto team_sum = [&](double v) {                        // workgroup sum, identical in every thread; one barrier
+        v = wave_sum(v);
+        if constexpr (NT == 64) return v;
+        double* rr = red + parity * (NT / 64);
+        parity ^= 1;
+        if (lane == 0) rr[tid >> 6] = v;
+        __syncthreads();
+        double s0 = rr[0];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w) s0 += rr[w];
+        return s0;
     };
 
     if (mode == 1) {                                       // compute_integral of bounds[t]
@@ -329,10 +410,14 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
     };
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
     const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));                 // (lower, fg]
+    stamp(2);
+    nodes += max(G.fix[2] - G.fix[0], 0);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
     const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+    stamp(3);
+    nodes += max(fixpos(nu) - fixpos(nl), 0);
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     double lo = __builtin_nan(""), hi = __builtin_nan("");
     int br = -1;                                           // bracket (tree) index; -1: NaN bracket (Q3)
@@ -342,20 +427,28 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
     if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; br = 3; }
     bool ustack = !(hi == P.sg0 || hi == P.sg1);
     int plo = br >= 0 ? fixpos(lo) : 0, phi = br >= 0 ? max(fixpos(hi), plo) : 0;
+    stamp(4);
     int h = 1;                                             // heap index of (lo, hi) in the bracket's tree
+    const int* tr = G.tree + (max(br, 0) << G.depth);
+    const int tsz = br >= 0 ? (1 << G.depth) : 0;          // tabulated heap nodes [1, tsz)
+    int pmt = tsz > 1 ? tr[1] : 0;                         // ub(mid) of heap node h, loaded a level ahead
 
     // ---- (iv) bisection (:250-309); Q2 / Q4 are resolved across dates by the finalize
     double prev = F, prevU = prevU0;
     int nt = -1, it = 0;
     uint64_t mask = 0;
     double* sn = snaps + t * P.stride;
-    for (; it < P.K && phi - plo > kSortTailCap; ++it) {
+    for (; it < P.K && phi - plo > TCAP; ++it) {
         const double mid = (lo + hi) / 2;
         if (tid == 0) sn[it] = mid;
         if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-        const bool tab = h < (1 << G.depth);               // tabulated; deeper: search (only if ties pile up)
-        const int pm = tab ? G.tree[(br << G.depth) + h] : sorted_ub(G.vs, plo, phi, mid);
+        const bool tab = h < tsz;                          // tabulated; deeper: search (only if ties pile up)
+        const int pm = tab ? pmt : sorted_ub(G.vs, plo, phi, mid);
+        const bool ctab = 2 * h + 1 < tsz;                 // both children tabulated: fetch them now,
+        const int pl = ctab ? tr[2 * h] : 0;               // their latency hides behind this level's slab
+        const int pr = ctab ? tr[2 * h + 1] : 0;
         const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
+        nodes += ustack ? pm - plo : phi - pm;
         const double slab_lower = ustack ? lo : mid;
         const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
         if (Fn != 0.0) mask |= (1ull << it);
@@ -363,11 +456,13 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
         if (ustack) { lo = mid; plo = pm; }
         else        { hi = mid; phi = pm; }
         if (tab) h = 2 * h + (ustack ? 1 : 0);             // children: (lo, mid) = 2h, (mid, hi) = 2h + 1
+        pmt = ustack ? pr : pl;
+        if (it < 15) stamp(5 + it);
         prev = Fn;
         prevU = mid;
     }
 
-    // ---- tail: the bracket's <= kSortTailCap nodes -> LDS, wave 0 finishes the levels
+    // ---- tail: the bracket's <= TCAP nodes -> LDS, wave 0 finishes the levels
     if (it < P.K) {
         const int tot = phi - plo;
         for (int e = tid; e < tot; e += NT) {
@@ -375,10 +470,12 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
             tail[e] = make_double2(G.vs[plo + e], fast ? node_fast(c) : node_generic(c));
         }
         __syncthreads();
+        stamp(29);
+        nodes += tot;
         if (tid < 64) {
-            double tx[kSortTailPerLane], ty[kSortTailPerLane];
+            double tx[TPL], ty[TPL];
 #pragma unroll
-            for (int m = 0; m < kSortTailPerLane; ++m) {
+            for (int m = 0; m < TPL; ++m) {
                 const bool ok = lane + 64 * m < tot;
                 const double2 e = ok ? tail[lane + 64 * m] : make_double2(__builtin_nan(""), 0.0);
                 tx[m] = e.x;
@@ -391,7 +488,7 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
                 const double a0 = ustack ? lo : mid, b0 = ustack ? mid : hi;   // slab (a0, b0]
                 double p = 0.0;
 #pragma unroll
-                for (int m = 0; m < kSortTailPerLane; ++m) p += (tx[m] > a0 && tx[m] <= b0) ? ty[m] : 0.0;
+                for (int m = 0; m < TPL; ++m) p += (tx[m] > a0 && tx[m] <= b0) ? ty[m] : 0.0;
                 const double val = wave_sum(p);
                 const double slab_lower = ustack ? lo : mid;
                 const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
@@ -404,6 +501,11 @@ __global__ __launch_bounds__(NT) void k_sorted(StaticDev S, SolveConst P, Sorted
         }
     }
 
+    stamp(31);
+    if (stamps && tid == 0) {
+        stamps[26] = __builtin_amdgcn_s_memrealtime();
+        stamps[28] = (unsigned long long)nodes;
+    }
     __shared__ int last;
     if (tid == 0) {
         sn[P.K] = (lo + hi) / 2;

@@ -12,11 +12,16 @@ out = sys.argv[1]
 args = sys.argv[2:]
 cfg = 2
 dates = 1000
-strategy = "direct"
+strategy = None
 for i, a in enumerate(args):
     if a == "--config": cfg = int(args[i + 1])
     if a == "--dates-per-gpu": dates = int(args[i + 1])
     if a == "--strategy": strategy = args[i + 1]
+if strategy in (None, "auto"):                       # bench.py's auto: COMPACT for 2 assets, SORTED for 3
+    strategy = "compact" if cfg == 2 else "sorted"   # engine.auto_strategy for configs 1-5
+dates = {1: 50, 2: 1000, 3: 5000, 4: 2000, 5: 5000}.get(cfg, dates)
+for i, a in enumerate(args):
+    if a == "--dates-per-gpu": dates = int(args[i + 1])
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
@@ -33,7 +38,7 @@ for k, d in sorted(summ.items()):
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {v:16.1f}")
-dom = {"prefix": "k_mass", "compact": "k_compact"}.get(strategy, "k_direct")
+dom = {"prefix": "k_mass", "compact": "k_compact", "sorted": "k_sorted"}.get(strategy, "k_direct")
 mass = [k for k in summ if re.search(rf"\b{dom}\b", k)]
 if mass:
     d = summ[mass[0]]

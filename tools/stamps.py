@@ -1,6 +1,6 @@
 """Phase breakdown of the DIRECT / COMPACT solve kernels from s_memtime stamps
 (diagnostic build aid).  Run on the GPU box:
-    python tools/stamps.py [--config 2] [--strategy direct|compact]"""
+    python tools/stamps.py [--config 2] [--strategy direct|compact|sorted]"""
 import os, sys
 import numpy as np
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "copula-msm-and-copula-garch-var_amd"),
@@ -28,11 +28,15 @@ st = buf.reshape(T, 32).astype(np.int64)
 if STRAT == "direct":
     names = ["tables", "rowsetup", "slab1", "slab2", "bracket"] + [f"it{i}" for i in range(it)]
     cols = list(range(6 + it))
-else:   # COMPACT: 0 start, 1 tables, 2 slab1, 3 slab2, 4 bracket, 5+it block levels, 29 tail build, 31 end
+else:   # COMPACT / SORTED: 0 start, 1 tables, 2 slab1, 3 slab2, 4 bracket, 5+it block levels, 29 tail build, 31 end
     rt = st[:, 25:27].copy()
     lev = [i for i in range(5, 20) if (st[:, i] != 0).any()]
     cols = [0, 1, 2, 3, 4] + lev + [29, 31]
     names = ["tables", "slab1", "slab2", "bracket"] + [f"lev{i - 5}" for i in lev] + ["tailbuild", "tail"]
+if STRAT == "sorted":
+    nodes = st[:, 28]
+    print(f"nodes evaluated per date: mean {nodes.mean():.0f} p50 {np.median(nodes):.0f} max {nodes.max()} "
+          f"(reachable {p.reach_nodes})")
 st = st[:, cols]
 for c in range(1, st.shape[1]):                 # dates that skipped a phase: zero length
     st[:, c] = np.where(st[:, c] == 0, st[:, c - 1], st[:, c])
