@@ -80,6 +80,8 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_solve": (i32, [v, C.POINTER(CvqSolveArgs), v, _ip, i32]),
         "cvq_snap_stride": (i32, [C.POINTER(CvqSolveArgs), _ip]),
         "cvq_solve_status": (i32, [v, _ip]),
+        "cvq_packed_block_len": (i32, [C.POINTER(CvqSolveArgs), i64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "cvq_solve_finalize_packed": (i32, [v, C.POINTER(CvqSolveArgs), v, i32, i64, i64, v]),
         "cvq_solve_local": (i32, [v, C.POINTER(CvqSolveArgs), v, v]),
         "cvq_solve_finalize": (i32, [v, C.POINTER(CvqSolveArgs), v, i32, v, i64, i64, v]),
         "cvq_msm_filter": (i32, [i32, i32, d, d, d, d, v, i64, i64, v, i32]),

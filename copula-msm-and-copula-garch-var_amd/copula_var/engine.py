@@ -194,6 +194,20 @@ class QuadraturePlan:
         N.check(N.lib().cvq_solve_local(self._h, C.byref(args), C.c_void_p(header_ptr), C.c_void_p(snaps_ptr)),
                 "cvq_solve_local")
 
+    @staticmethod
+    def packed_block_len(args: N.CvqSolveArgs, dates_per_rank: int) -> Tuple[int, int]:
+        """(block length, header offset) in doubles of one rank's packed block."""
+        ln, off = C.c_int64(), C.c_int64()
+        N.check(N.lib().cvq_packed_block_len(C.byref(args), int(dates_per_rank), C.byref(ln), C.byref(off)),
+                "cvq_packed_block_len")
+        return int(ln.value), int(off.value)
+
+    def solve_finalize_packed(self, args: N.CvqSolveArgs, blocks_ptr: int, n_ranks: int, dates_per_rank: int,
+                              T_total: int, var_ptr: int) -> None:
+        N.check(N.lib().cvq_solve_finalize_packed(self._h, C.byref(args), C.c_void_p(blocks_ptr), int(n_ranks),
+                                                  int(dates_per_rank), int(T_total), C.c_void_p(var_ptr)),
+                "cvq_solve_finalize_packed")
+
     def solve_finalize(self, args: N.CvqSolveArgs, headers_ptr: int, n_ranks: int, snaps_ptr: int,
                        dates_per_rank: int, T_total: int, var_ptr: int) -> None:
         N.check(N.lib().cvq_solve_finalize(self._h, C.byref(args), C.c_void_p(headers_ptr), int(n_ranks),

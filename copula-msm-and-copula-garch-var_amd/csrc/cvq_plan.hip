@@ -1120,6 +1120,37 @@ int32_t cvq_solve_finalize(cvq_plan* p, const cvq_solve_args* a, const void* d_h
     return CVQ_OK;
 }
 
+int32_t cvq_packed_block_len(const cvq_solve_args* a, int64_t dates_per_rank, int64_t* len, int64_t* header_offset) {
+    CVQ_REQUIRE(a != nullptr && len != nullptr && dates_per_rank >= 1, CVQ_ERR_INVALID, "bad argument");
+    int32_t stride;
+    int rc = cvq_snap_stride(a, &stride);
+    if (rc) return rc;
+    const int64_t hoff = (dates_per_rank * stride + 1) & ~(int64_t)1;    // 16-B aligned header
+    *len = hoff + 2;
+    if (header_offset) *header_offset = hoff;
+    return CVQ_OK;
+}
+
+int32_t cvq_solve_finalize_packed(cvq_plan* p, const cvq_solve_args* a, const double* d_blocks, int32_t n_ranks,
+                                  int64_t dates_per_rank, int64_t T_total, double* d_var) {
+    CVQ_REQUIRE(p != nullptr && a != nullptr && d_blocks && d_var, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(n_ranks >= 1 && dates_per_rank >= 1 && T_total <= (int64_t)n_ranks * dates_per_rank, CVQ_ERR_INVALID,
+                "T_total exceeds n_ranks * dates_per_rank");
+    CVQ_REQUIRE(((uintptr_t)d_blocks & 15) == 0, CVQ_ERR_INVALID, "packed blocks must be 16-byte aligned");
+    int32_t stride;
+    int64_t len, hoff;
+    int rc = cvq_snap_stride(a, &stride);
+    if (rc || (rc = cvq_packed_block_len(a, dates_per_rank, &len, &hoff))) return rc;
+    CVQ_HIP_CHECK(hipSetDevice(p->device));
+    const unsigned blocks = (unsigned)std::max<long long>(1, (T_total + 255) / 256);
+    TimedScope ts(p, TK_FINALIZE);
+    hipLaunchKernelGGL(k_finalize_packed, dim3(blocks), dim3(256), 0, p->stream, d_blocks, n_ranks,
+                       (long long)dates_per_rank, (long long)len, (long long)hoff, (long long)T_total, stride,
+                       stride - 1, a->ptf_mean, d_var, p->d_err);
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
 int32_t cvq_solve_status(cvq_plan* p, int32_t* iters_out) {
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
     CVQ_HIP_CHECK(hipSetDevice(p->device));

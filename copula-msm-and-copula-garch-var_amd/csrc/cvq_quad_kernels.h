@@ -511,6 +511,31 @@ __global__ void k_finalize(const Header* __restrict__ hdrs, int nranks, const do
     if (t >= T_total) return;
     var[t] = snaps[t * stride + kstop] + ptf_mean;
 }
+
+// Same, from ONE all-gathered buffer of per-rank blocks (cvq_solve_finalize_packed):
+// block r = blocks + r * rstride holds the rank's [per][stride] snapshots, then its
+// 16-B header at offset hoff (doubles, 16-B aligned).
+__global__ void k_finalize_packed(const double* __restrict__ blocks, int nranks, long long per, long long rstride,
+                                  long long hoff, long long T_total, int stride, int K, double ptf_mean,
+                                  double* __restrict__ var, int* __restrict__ err) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    int N = 0, e = 0;
+    unsigned long long nz = 0;
+    for (int r = 0; r < nranks; ++r) {
+        const Header* h = (const Header*)(blocks + r * rstride + hoff);
+        N = max(N, h->iters);
+        e |= h->error;
+        nz |= h->nonzero;
+    }
+    if (N > K) e |= 2;
+    int kstop = min(N, K);
+    for (int k = 0; k < kstop; ++k)
+        if (!((nz >> k) & 1ull)) { kstop = k; break; }
+    if (t == 0) { err[0] = e; err[1] = kstop; err[2] = N; }
+    if (t >= T_total) return;
+    const long long r = t / per;
+    var[t] = blocks[r * rstride + (t - r * per) * stride + kstop] + ptf_mean;
+}
 #endif
 
 }  // namespace cvq

@@ -148,13 +148,23 @@ int32_t cvq_solve_status(cvq_plan* plan, int32_t* iters_out);
 /* Sharded solve, for one process per GPU (date blocks).
  * Phase 1 (local):  per-date bisection snapshots + a 16-byte header
  *   d_header: 16 bytes device, d_snaps: [T_local][cvq_snap_stride(args)] device.
- * Exchange: the caller all-gathers headers and snaps (RCCL).
+ * Exchange: the caller all-gathers headers and snaps (RCCL) -- or, packed, one buffer.
  * Phase 2: finalise every date from the gathered blocks; d_var [T_total] device. */
 int32_t cvq_snap_stride(const cvq_solve_args* args, int32_t* stride);
 int32_t cvq_solve_local(cvq_plan* plan, const cvq_solve_args* args, void* d_header, double* d_snaps);
 int32_t cvq_solve_finalize(cvq_plan* plan, const cvq_solve_args* args, const void* d_headers,
                            int32_t n_ranks, const double* d_snaps, int64_t dates_per_rank,
                            int64_t T_total, double* d_var);
+/* Packed variant for ONE all-gather per solve: each rank's block is its snapshots
+ * [dates_per_rank][stride] followed by its 16-byte header at header_offset (doubles;
+ * cvq_solve_local's d_snaps = block, d_header = block + header_offset), block length
+ * len doubles (even, so blocks stay 16-byte aligned).  d_blocks = [n_ranks][len],
+ * 16-byte aligned. */
+int32_t cvq_packed_block_len(const cvq_solve_args* args, int64_t dates_per_rank, int64_t* len,
+                             int64_t* header_offset);
+int32_t cvq_solve_finalize_packed(cvq_plan* plan, const cvq_solve_args* args, const double* d_blocks,
+                                  int32_t n_ranks, int64_t dates_per_rank, int64_t T_total,
+                                  double* d_var);
 
 /* ------------------------------------------------ per-date forecast stage */
 /* MSM forecasts_array (msm_estimation.py:140-202 -> calc_marginals.py:33-38 ->

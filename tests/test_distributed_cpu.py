@@ -55,7 +55,9 @@ def _worker(rank, world, port, case, q):
             hdr[1] = nz if nz < (1 << 63) else nz - (1 << 64)
             snaps[: sn.shape[0]] = torch.from_numpy(sn)
 
-        def finalize(hdr_all, snaps_all, var):
+        def finalize(blocks, var):                        # the gathered [world, block_len] blocks
+            hdr_all = blocks[:, s.hdr_off: s.hdr_off + 2].contiguous().view(torch.int64)
+            snaps_all = blocks[:, : per * (K + 1)].reshape(world * per, K + 1)
             h = hdr_all.numpy().reshape(-1, 2)
             headers = [(int(a) & 0xFFFFFFFF, int(a) >> 32, int(b) & ((1 << 64) - 1)) for a, b in h]
             v, _, err = S.finalize(headers, snaps_all.numpy(), T, K, ptf)

@@ -123,3 +123,39 @@ def test_non_dyadic_guesses_device_mode(strategy):
         assert np.array_equal(s.solve().cpu().numpy(), ref)
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("strategy", ["compact", "sorted"])
+@pytest.mark.parametrize("case,ranks", [("cfg1", 3), ("cfg2_n64", 2), ("cfg4_k6_n16", 2)])
+def test_packed_single_gather_layout(case, ranks, strategy):
+    """cvq_solve_finalize_packed: every rank's snapshots + header in ONE block, the blocks
+    concatenated as one all-gather lays them out; every rank's finalize gives the batch VaR."""
+    from copula_var import engine
+    from copula_var.distributed import shard
+    from copula_var.engine import QuadraturePlan
+    z = load_golden(case)
+    if strategy == "compact" and int(z["dim"]) != 2:
+        pytest.skip("COMPACT is built for dim == 2")
+    T = z["var"].size
+    args = engine.solve_args(float(z["ptf_mean"]))
+    per = shard(T, 0, ranks)[2]
+    ln, off = QuadraturePlan.packed_block_len(args, per)
+    assert ln % 2 == 0 and off % 2 == 0 and off >= per * QuadraturePlan.snap_stride(args)
+    blocks = torch.full((ranks, ln), float("nan"), dtype=torch.float64, device="cuda")
+    plans = []
+    try:
+        for r in range(ranks):
+            lo, hi, _ = shard(T, r, ranks)
+            p = _plan(z, slice(lo, hi), strategy)
+            plans.append(p)
+            blk = blocks[r]
+            blk[off: off + 2] = 0.0
+            p.solve_local(args, blk[off:].data_ptr(), blk.data_ptr())
+        for p in plans:
+            var = torch.empty(T, dtype=torch.float64, device="cuda")
+            p.solve_finalize_packed(args, blocks.data_ptr(), ranks, per, T, var.data_ptr())
+            assert p.solve_status() == int(z["n_calls"]) - 2
+            assert np.array_equal(var.cpu().numpy(), z["var"])
+    finally:
+        for p in plans:
+            p.close()
