@@ -123,11 +123,17 @@ inline size_t sorted_lds_bytes(int n, int nt, int dim) {
 // mode 0: calc_var solve (snapshots + header, fused finalize when P.fin_var);
 // mode 1: one slab per date (compute_integral): out[t] = I_t(bounds[2t], bounds[2t+1]].
 // Minimum waves per SIMD asked of the register allocator: 5 for 2-D (measured
-// +15% on config 5, neutral on 2), none for 3-D (its exp chain needs the registers).
+// +15% on config 5, neutral on 2), 4 for 3-D (<= 128 VGPRs; its exp chain sits at
+// that boundary, and 5 measured slower).
 #ifndef CVQ_SORT_MIN_WAVES2
 #define CVQ_SORT_MIN_WAVES2 5
 #endif
-__host__ __device__ constexpr int sorted_min_waves(int dim) { return dim == 2 ? CVQ_SORT_MIN_WAVES2 : 1; }
+#ifndef CVQ_SORT_MIN_WAVES3
+#define CVQ_SORT_MIN_WAVES3 4
+#endif
+__host__ __device__ constexpr int sorted_min_waves(int dim) {
+    return dim == 2 ? CVQ_SORT_MIN_WAVES2 : CVQ_SORT_MIN_WAVES3;
+}
 
 template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED>
 __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
