@@ -394,8 +394,8 @@ void build_vstar(const std::vector<double>& x, double w0, double w1, std::vector
 }
 
 // SORTED: every reachable node (row r, inner j in [1, kmax_r]) with its v*, sorted
-// by (v*, packed index); packed = i0 | j << 16 (2-D), a0 | i1 << 9 | j << 17 (3-D) with
-// a0 = i0 + n on the plane i1 == 0 (the Q6 plane has its own axis-0 records).
+// by (v*, packed word); the word holds the LDS offsets of the node's records in the
+// kernel's layout for (dim, n) (sorted_pack, cvq_sorted_kernels.h).
 void build_sorted_nodes(const std::vector<double>& x, const StaticDev& S, const std::vector<int>& kmax,
                         std::vector<double>& vs, std::vector<uint32_t>& idx) {
     const int n = S.n;
@@ -404,9 +404,9 @@ void build_sorted_nodes(const std::vector<double>& x, const StaticDev& S, const 
     for (int r = 0; r < S.nrows; ++r) {
         const int i0 = S.dim == 2 ? r : r / n, i1 = S.dim == 2 ? 0 : r % n;
         const double lev = S.dim == 2 ? x[i0] * S.w1 : x[i0] * S.w1 + x[i1] * S.w2;   // integration_algo.py:20
-        const uint32_t base = S.dim == 2 ? (uint32_t)i0 : (uint32_t)((i0 + (i1 == 0 ? n : 0)) | (i1 << 9));
-        const int jsh = S.dim == 2 ? 16 : 17;
-        for (int j = 1; j <= kmax[r]; ++j) nodes.emplace_back(vstar_exact(x[j], lev, S.w0), base | ((uint32_t)j << jsh));
+        const int lay = sorted_layout(S.dim, n);
+        for (int j = 1; j <= kmax[r]; ++j)
+            nodes.emplace_back(vstar_exact(x[j], lev, S.w0), sorted_pack(lay, n, i0, i1, j));
     }
     std::sort(nodes.begin(), nodes.end());
     vs.resize(nodes.size());

@@ -27,11 +27,21 @@ struct SortedLaunch {
     double* stamps;
 };
 
-template <int COP, bool MSM, int DIM, int PM, bool FUSED>
-void launch_f(const SortedLaunch& L) {
-    hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED>), dim3((unsigned)L.T), dim3(kSortNT),
+template <int COP, bool MSM, int DIM, int PM, bool FUSED, int LAY>
+void launch_l(const SortedLaunch& L) {
+    hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY>), dim3((unsigned)L.T), dim3(kSortNT),
                        sorted_lds_bytes(L.S.n, kSortNT, DIM), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode,
                        L.bounds, L.out, L.snaps, L.hdr, L.stamps);
+}
+
+template <int COP, bool MSM, int DIM, int PM, bool FUSED>
+void launch_f(const SortedLaunch& L) {
+    if constexpr (DIM == 2) {
+        launch_l<COP, MSM, DIM, PM, FUSED, kLay2>(L);
+    } else {
+        if (sorted_layout(DIM, L.S.n) == kLay3F) launch_l<COP, MSM, DIM, PM, FUSED, kLay3F>(L);
+        else launch_l<COP, MSM, DIM, PM, FUSED, kLay3G>(L);
+    }
 }
 
 template <int COP, bool MSM, int DIM, int PM>

@@ -91,13 +91,48 @@ __device__ __forceinline__ int sorted_ub(const double* __restrict__ vs, int lo, 
     return lo;
 }
 
-// a0: axis-0 record index (3-D: i0 + n on the plane i1 == 0), i1, j
-template <int DIM>
-__device__ __forceinline__ void unpack_node(uint32_t c, int* a0, int* i1, int* j) {
-    if constexpr (DIM == 2) {
-        *a0 = (int)(c & 0xFFFFu);
+// Node words and LDS layouts.  The host packs LDS byte offsets of a node's records into
+// its 32-bit word, so the node loop spends 1-2 integer ops per record address:
+//   kLay2   (2-D): off0 | off2 << 16, absolute byte offsets (the kernel's LDS starts at 0)
+//   kLay3F  (3-D, n <= 128, fixed layout): axis-0 record a0 in bits 4-11 (a0 * 16),
+//           i1 in bits 12-18 (32-B axis-1 records), j in bits 25-31 (j * 16)
+//   kLay3G  (3-D, n <= 255): a0 | i1 << 9 | j << 17, record indices
+// with a0 = i0 + n on the plane i1 == 0 (Q6), whose axis-0 records are separate.
+enum { kLay2 = 0, kLay3F = 1, kLay3G = 2 };
+constexpr int kLay3FMaxN = 128;
+constexpr int kLay3FAx1 = 4096, kLay3FAx2 = 8192, kLay3FBytes = 10240;   // byte offsets / size of its region
+__host__ __device__ constexpr int sorted_layout(int dim, int n) {
+    return dim == 2 ? kLay2 : (n <= kLay3FMaxN ? kLay3F : kLay3G);
+}
+inline uint32_t sorted_pack(int layout, int n, int i0, int i1, int j) {
+    const int ns = (n + 1) & ~1;
+    const int a0 = i0 + (layout != kLay2 && i1 == 0 ? n : 0);
+    if (layout == kLay2) return (uint32_t)(16 * i0) | ((uint32_t)(16 * (ns + j)) << 16);
+    if (layout == kLay3F) return ((uint32_t)a0 << 4) | ((uint32_t)i1 << 12) | ((uint32_t)j << 25);
+    return (uint32_t)a0 | ((uint32_t)i1 << 9) | ((uint32_t)j << 17);
+}
+// LDS read at an absolute byte address (the packed offsets, valid because the kernel has no
+// static LDS: its dynamic region starts at address 0 -- checked at kernel start).  Going
+// through the extern array instead adds its (link-time, zero) address to every record.
+typedef __attribute__((address_space(3))) const double lds_f64;
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const f64x2_t lds_f64x2;
+__device__ __forceinline__ const lds_f64* lds_at(uint32_t byte_off) { return (const lds_f64*)(size_t)byte_off; }
+__device__ __forceinline__ uint32_t lds_base(const double* p) {
+    return (uint32_t)(size_t)(__attribute__((address_space(3))) const double*)p;
+}
+
+// record indices (a0, i1, j) of a node word (the generic path's view)
+template <int LAY>
+__device__ __forceinline__ void unpack_node(uint32_t c, int ns, int* a0, int* i1, int* j) {
+    if constexpr (LAY == kLay2) {
+        *a0 = (int)(c & 0xFFFFu) >> 4;
         *i1 = 0;
-        *j = (int)(c >> 16);
+        *j = ((int)(c >> 16) >> 4) - ns;
+    } else if constexpr (LAY == kLay3F) {
+        *a0 = (int)__builtin_amdgcn_ubfe(c, 4, 8);
+        *i1 = (int)__builtin_amdgcn_ubfe(c, 12, 7);
+        *j = (int)(c >> 25);
     } else {
         *a0 = (int)__builtin_amdgcn_ubfe(c, 0, 9);
         *i1 = (int)__builtin_amdgcn_ubfe(c, 9, 8);
@@ -113,11 +148,16 @@ __device__ __forceinline__ void unpack_node(uint32_t c, int* a0, int* i1, int* j
 // work they save (measured).
 // largest n the kernel's register tables hold: the plan's 512 in 2-D, the 8-bit packing's 255 in 3-D
 __host__ __device__ constexpr int sorted_max_n(int dim) { return dim == 2 ? 512 : 255; }
-__host__ __device__ constexpr int sorted_region(int dim) { return dim == 2 ? 6 : 9; }
 inline int sorted_stride(int n) { return (n + 1) & ~1; }
+// doubles of the table region
+__host__ __device__ inline int sorted_region_doubles(int layout, int n) {
+    const int ns = (n + 1) & ~1;
+    return layout == kLay2 ? 6 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
+}
+constexpr int kSortScalars = 4;                // flags, arest, last (+ pad), after the reduction slots
 inline size_t sorted_lds_bytes(int n, int nt, int dim) {
-    return sizeof(double) * (size_t)sorted_region(dim) * sorted_stride(n) + sizeof(double2) * sorted_tail_cap(dim) +
-           sizeof(double) * 2 * (nt / 64);
+    return sizeof(double) * ((size_t)sorted_region_doubles(sorted_layout(dim, n), n) + 2 * (nt / 64) + kSortScalars) +
+           sizeof(double2) * sorted_tail_cap(dim);
 }
 
 // mode 0: calc_var solve (snapshots + header, fused finalize when P.fin_var);
@@ -135,7 +175,7 @@ __host__ __device__ constexpr int sorted_min_waves(int dim) {
     return dim == 2 ? CVQ_SORT_MIN_WAVES2 : CVQ_SORT_MIN_WAVES3;
 }
 
-template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED>
+template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY>
 __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
@@ -149,17 +189,23 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     // One LDS region holds EITHER the generic tables (reference semantics: z, B, w per
     // axis; axis 0 of 3-D: w = the i1 == 0 weight) OR the fast records (16 B per axis
     // entry; 3-D axis 0 twice, [n, 2n) = the plane i1 == 0), chosen per date.
+    // (no static __shared__ variables: the dynamic region starts at LDS address 0, so the
+    // host-packed record offsets are addresses)
     double* zg = lds;                              // generic [DIM][n]
     double* Bg = zg + DIM * ns;                    // generic [DIM][n]
     double* wg = Bg + DIM * ns;                    // generic [DIM][n]
     double* fr0 = lds;                             // fast [ns (3-D: 2 ns)][2] axis 0
-    double* fr1 = fr0 + (DIM == 3 ? 4 : 2) * ns;   // fast [ns][2] axis 1 (3-D)
-    double* fg1 = fr1 + (DIM == 3 ? 2 : 0) * ns;   // fast [ns] axis 1, third value (3-D)
-    double* fr2 = fg1 + (DIM == 3 ? 1 : 0) * ns;   // fast [ns][2] inner axis
-    double2* tail = (double2*)(lds + sorted_region(DIM) * ns);   // [TCAP] (v*, value)
+    // axis 1 (3-D): kLay3F 32-B records (c01 z1, c12 z1, g1 | z1, B'1); kLay3G [ns][2] + fg1 [ns]
+    double* fr1 = LAY == kLay3F ? lds + kLay3FAx1 / 8 : fr0 + (DIM == 3 ? 4 : 2) * ns;
+    double* fg1 = LAY == kLay3F ? fr1 + 2 : fr1 + (DIM == 3 ? 2 : 0) * ns;
+    constexpr int R1 = LAY == kLay3F ? 4 : 2;      // doubles per axis-1 record
+    constexpr int FG = LAY == kLay3F ? 4 : 1;      // fg1 stride
+    double* fr2 = LAY == kLay3F ? lds + kLay3FAx2 / 8 : fg1 + (DIM == 3 ? 1 : 0) * ns;   // fast [ns][2] inner axis
+    double2* tail = (double2*)(lds + sorted_region_doubles(LAY, n));   // [TCAP] (v*, value)
     double* red = (double*)(tail + TCAP);          // [2][NT / 64] reduction slots
-    __shared__ int flags;                          // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
-    __shared__ double s_arest;                     // 3-D: the axis-0 weight off the plane i1 == 0
+    int& flags = *(int*)(red + 2 * (NT / 64));     // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
+    double& s_arest = *(red + 2 * (NT / 64) + 1);  // 3-D: the axis-0 weight off the plane i1 == 0
+    int& last = *(int*)(red + 2 * (NT / 64) + 2);  // fused finalize: this workgroup is the last
 
     // diagnostic phase stamps (CVQ_STAMPS=1, never in a timed run): COMPACT's slots --
     // 0 start, 1 tables, 2 first slab, 3 second slab, 4 bracket, 5 + level, 29 tail
@@ -226,11 +272,12 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         }
         s_arest = s0;
     }
+    if (tid == 0 && lds_base(lds) != 0) bad |= 4;          // packed offsets need the region at LDS 0
     if (bad) atomicOr(&flags, bad);
     __syncthreads();
     const int fl = flags;
     const bool rank1 = !(fl & 2);
-    const bool fast = rank1 && !(fl & 1);
+    const bool fast = rank1 && !(fl & 5);
     const double arest = DIM == 3 ? s_arest : 1.0;
     // Gaussian: -z^T R^-1 z / 2 = sum_c -Ri_cc z_c^2 / 2 + c01 z0 z1 + c02 z0 z2 + c12 z1 z2;
     // Student: 1 + z^T R^-1 z / nu = 1 + sum_c a_cc z_c^2 + a01 z0 z1 + a02 z0 z2 + a12 z1 z2
@@ -266,14 +313,14 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
                 fr2[2 * i] = z;
                 fr2[2 * i + 1] = lg(B * w) + kcc;
             } else {
-                fr1[2 * i] = k01 * z;
-                fr1[2 * i + 1] = k12 * z;
-                fg1[i] = lg(B * w) + kcc;
+                fr1[R1 * i] = k01 * z;
+                fr1[R1 * i + 1] = k12 * z;
+                fg1[FG * i] = lg(B * w) + kcc;
             }
         } else {                                           // Student: z and scale; Plackett: u and scale
             const double sc = (ax == 0 && COP == CVQ_STUDENT ? S.term1 : 1.0) * B *
                               (ax == 0 && DIM == 3 ? arest : w);
-            double* r = (ax == 0 ? fr0 : ax == DIM - 1 ? fr2 : fr1) + 2 * i;
+            double* r = ax == 0 ? fr0 + 2 * i : ax == DIM - 1 ? fr2 + 2 * i : fr1 + R1 * i;
             r[0] = z;
             r[1] = sc;
             if (DIM == 3 && ax == 0) {                                       // plane i1 == 0 (Q6)
@@ -288,17 +335,36 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     stamp(1);
     // Student: b = 1 + z^T R^-1 z / nu = 1 + z0 (a00 z0 + k01 z1 + k02 z2) + z1 (a11 z1 + k12 z2) + a22 z2^2
     const double a00 = kq * S.Ri[0], a11 = kq * S.Ri[DIM + 1], a22 = kq * S.Ri[DIM * DIM - 1];
+    // LDS records of a node word (host-packed offsets, see sorted_pack)
+    auto rd2 = [](const lds_f64* r) {                  // one ds_read_b128
+        const f64x2_t v = *(const lds_f64x2*)r;
+        return make_double2(v.x, v.y);
+    };
+    auto rec0 = [&](uint32_t c) -> const lds_f64* {
+        if constexpr (LAY == kLay2) return lds_at(c & 0xFFFFu);
+        else if constexpr (LAY == kLay3F) return lds_at(c & 0xFF0u);
+        else return lds_at(lds_base(fr0) + 16 * __builtin_amdgcn_ubfe(c, 0, 9));
+    };
+    auto rec1 = [&](uint32_t c) -> const lds_f64* {
+        if constexpr (LAY == kLay3F) return lds_at(kLay3FAx1 + ((c >> 7) & 0xFE0u));
+        else return lds_at(lds_base(fr1) + 16 * __builtin_amdgcn_ubfe(c, 9, 8));
+    };
+    auto rec2 = [&](uint32_t c) -> const lds_f64* {
+        if constexpr (LAY == kLay2) return lds_at(c >> 16);
+        else if constexpr (LAY == kLay3F) return lds_at(kLay3FAx2 + (c >> 21));
+        else return lds_at(lds_base(fr2) + 16 * (c >> 17));
+    };
     auto node_fast = [&](uint32_t c) -> double {
-        int a0, i1, j;
-        unpack_node<DIM>(c, &a0, &i1, &j);
-        const double2 A = *(const double2*)(fr0 + 2 * a0);
-        const double2 C = *(const double2*)(fr2 + 2 * j);
+        const double2 A = rd2(rec0(c));
+        const double2 C = rd2(rec2(c));
         if constexpr (COP == CVQ_GAUSSIAN) {
             if constexpr (DIM == 2) {
                 return exp_node(fma(A.x, C.x, A.y + C.y));
             } else {
-                const double2 Bv = *(const double2*)(fr1 + 2 * i1);
-                return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + fg1[i1]) + C.y)));
+                const lds_f64* r1 = rec1(c);
+                const double2 Bv = rd2(r1);
+                const double g1 = LAY == kLay3F ? r1[2] : fg1[__builtin_amdgcn_ubfe(c, 9, 8)];
+                return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
             }
         } else if constexpr (COP == CVQ_STUDENT) {
             double b, sc;
@@ -306,7 +372,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
                 b = fma(A.x, fma(a00, A.x, k02 * C.x), fma(a22 * C.x, C.x, 1.0));
                 sc = A.y * C.y;
             } else {
-                const double2 Bv = *(const double2*)(fr1 + 2 * i1);
+                const double2 Bv = rd2(rec1(c));
                 b = fma(A.x, fma(a00, A.x, fma(k01, Bv.x, k02 * C.x)), fma(Bv.x, fma(a11, Bv.x, k12 * C.x),
                                                                               fma(a22 * C.x, C.x, 1.0)));
                 sc = (A.y * Bv.y) * C.y;
@@ -328,7 +394,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     };
     auto node_generic = [&](uint32_t c) -> double {
         int i0, i1, j;
-        unpack_node<DIM>(c, &i0, &i1, &j);
+        unpack_node<LAY>(c, ns, &i0, &i1, &j);
         if (DIM == 3 && i0 >= n) i0 -= n;                  // the plane's axis-0 record index
         const double zi = zg[(DIM - 1) * n + j], Bi = Bg[(DIM - 1) * n + j];
         double W;
@@ -512,7 +578,6 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         stamps[26] = __builtin_amdgcn_s_memrealtime();
         stamps[28] = (unsigned long long)nodes;
     }
-    __shared__ int last;
     if (tid == 0) {
         sn[P.K] = (lo + hi) / 2;
         if (nt < 0 && !(hi - lo > P.tol)) nt = P.K;

@@ -182,3 +182,29 @@ def test_sorted_rejects_levels_above_v_cap():
             p.compute_integral(np.tile([-1.0, 0.5], (z["var"].size, 1)))
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("copula", ["student", "gaussian"])
+def test_3d_general_layout_n_above_128(copula):
+    """3-D with n in (128, 255] takes the general node-word layout (kLay3G); GARCH
+    margins (Q = 1) keep the oracle cheap at n = 136."""
+    from copula_var import synthetic, tables
+    from oracle.quadrature import calc_var
+    R3 = np.array([[1.0, 0.5, 0.4], [0.5, 1.0, 0.3], [0.4, 0.3, 1.0]])
+    c = synthetic.Config("g3_136", "garch", copula, 3, 136, 3, garch_params=[{"omega": 0.05, "alpha": 0.08,
+                                                                             "beta": 0.90}] * 3,
+                         nu=6.0, corr=R3, innov_copula="gaussian", innov_corr=R3)
+    rets = synthetic.simulate_returns(c)
+    _, ptf, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
+    ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
+    P = _problem(c, ipt, uvs, ggp)
+    ref, ref_it, _ = calc_var(P.compute_integral, P.T, ptf)
+    p = _plan(c, ipt, uvs, ggp, "sorted")
+    try:
+        var, it = p.calc_var(ptf)
+        b = np.tile([-3.0, -2.0], (P.T, 1))
+        np.testing.assert_allclose(p.compute_integral(b), P.compute_integral(b), rtol=SLAB_RTOL, atol=SLAB_ATOL)
+    finally:
+        p.close()
+    assert it == ref_it
+    assert np.array_equal(var, ref)

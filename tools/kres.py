@@ -10,7 +10,8 @@ for line in sys.stdin:
         cur = {"name": m.group(1)}
         rows.append(cur)
         continue
-    m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+)", line)
+    m = re.search(r"\b(VGPRs|AGPRs|SGPRs|TotalSGPRs|VGPRs Spill|SGPRs Spill|Occupancy \[waves/SIMD\]|"
+                  r"LDS Size \[bytes/block\]): (\d+)", line)
     if m and cur is not None:
         cur[m.group(1).strip()] = int(m.group(2))
 for r in rows:
