@@ -81,6 +81,29 @@ __device__ __forceinline__ double exp_node(double x) {
     return __builtin_amdgcn_ldexp(p, (int)k);
 }
 
+// b^-(m/2) for the fast path's b = 1 + z^T R^-1 z / nu: the fast path requires finite
+// |z| < 1e15 and R is positive definite, so 1 <= b < ~1e31 and b^(m/2) stays finite:
+// pow_node_t's overflow guard is dropped (PM > 0: squarings, v_rcp_f64 + one Newton
+// step, ~1e-15 relative).
+template <int PM>
+__device__ __forceinline__ double pow_fast(double b, int m, double ex) {
+    if constexpr (PM == 0) {
+        return pow_node(b, m, ex);
+    } else {
+        constexpr int k = PM >> 1;
+        double r = 1.0, s2 = b;
+#pragma unroll
+        for (int bit = 0; bit < 6; ++bit) {
+            if ((k >> bit) & 1) r *= s2;
+            if ((k >> (bit + 1)) == 0) break;
+            s2 *= s2;
+        }
+        if constexpr (PM & 1) r *= sqrt(b);
+        const double y = __builtin_amdgcn_rcp(r);
+        return fma(y, fma(-r, y, 1.0), y);
+    }
+}
+
 // upper bound: first position p in [lo, hi) with vs[p] > v (hi if none); NaN v -> lo.
 __device__ __forceinline__ int sorted_ub(const double* __restrict__ vs, int lo, int hi, double v) {
     if (!(v == v)) return lo;
@@ -250,6 +273,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
             }
             if (!isfinite(A) || !isfinite(B)) bad |= 1;
             if (!(B * w > 0.0)) bad |= 1;                  // fast records take logs of B w
+            if (!(fabs(A) < 1.0e15)) bad |= 1;             // fast powers / exps need a bounded quadratic form
             eA[k][ax] = A;
             eB[k][ax] = B;
             eW[k][ax] = w;
@@ -377,7 +401,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
                                                                               fma(a22 * C.x, C.x, 1.0)));
                 sc = (A.y * Bv.y) * C.y;
             }
-            return sc * pow_node_t<PM>(b, S.node_m, S.node_ex);
+            return sc * pow_fast<PM>(b, S.node_m, S.node_ex);
         } else {                                           // Plackett (plackett.py:66-69, Q11), 2-D
             const double th = S.theta, a1 = th - 1.0, u = A.x, v = C.x, s2 = u + v;
             const double num = th * fma(a1, fma(-2.0 * u, v, s2), 1.0);
