@@ -46,7 +46,10 @@ namespace cvq {
 __host__ __device__ constexpr int sorted_tail_per_lane(int dim) { return dim == 2 ? CVQ_SORT_TAIL2 : CVQ_SORT_TAIL3; }
 __host__ __device__ constexpr int sorted_tail_cap(int dim) { return 64 * sorted_tail_per_lane(dim); }
 constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisection level
-constexpr int kSortIlp = 4;                           // nodes in flight per thread
+#ifndef CVQ_SORT_ILP
+#define CVQ_SORT_ILP 4
+#endif
+constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
 
 // Date-independent device tables of a SORTED plan.
 struct SortedGeom {
@@ -476,7 +479,11 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         } else {
             for (; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
         }
-        return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+#pragma unroll
+        for (int h = 1; h < kSortIlp; h <<= 1)
+#pragma unroll
+            for (int u = 0; u + h < kSortIlp; u += 2 * h) acc[u] += acc[u + h];
+        return acc[0];
     };
     int parity = 0;
     auto team_sum = [&](double v) {                        // workgroup sum, identical in every thread; one barrier
