@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--cpu-dates", type=int, default=0,
                     help="CPU sample size (0 = four per worker: ~15 s of joblib work on config 2)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
-    ap.add_argument("--e2e", type=int, default=0, help="also time the device forecast stage")
+    ap.add_argument("--e2e", type=int, default=1,
+                    help="MSM, 1 GPU: also time end-to-end steps (device forecast tables + solve, from returns)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="independent batches in flight (one plan + HIP stream each); 1 = one batch at a time")
     ap.add_argument("--time-all", type=int, default=0,
@@ -192,6 +193,10 @@ def main():
             traffic = None
     kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items() if v[1]}
 
+    e2e = None
+    if a.e2e and c.model == "msm" and world == 1:
+        e2e = end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev)
+
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
         cpu = cpu_baseline(c, ipt, uvs, ggp, ptf_mean, vals, a)
@@ -227,6 +232,7 @@ def main():
                                   "frac": fp64_tflops / FP64_PEAK_TFLOPS, "flop_per_node": flop_node}},
             "kernels": kernels,
             "forecast_stage_s": t_fc,
+            "e2e": e2e,
             "var_checksum": float(np.nansum(vals)),
             "var_nan": int(np.isnan(vals).sum()),
             "cpu_baseline": cpu,
@@ -236,6 +242,44 @@ def main():
         p.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):
+    """End-to-end steps: centred returns resident in HBM -> every asset's
+    rolling-window MSM filters, state collapse and forecast combinations on the device
+    (cvq_msm_tables) -> the solve reading those tables in place.  Same batches in flight;
+    the VaR must equal the main loop's (tables resident) bit for bit."""
+    import torch
+    from copula_var import engine, tables
+    vsa = np.array([tables.msm_vol_states(c.k, p["m_0"], p["sig"]) for p in c.msm_params])
+    smap, uvs = tables.unique_vol_map(vsa)
+    prm = [[p["m_0"], p["sig"], p["b"], p["gamma"]] for p in c.msm_params]
+    r_dev = torch.tensor(np.ascontiguousarray(block[:-1].T), dtype=torch.float64, device=dev)
+    nf = len(plans)
+    mts = [engine.MsmTables(prm, c.k, smap, uvs.shape[1], c.n_in, per, dev.index or 0) for _ in range(nf)]
+
+    def step(i):
+        k = i % nf
+        with torch.cuda.stream(streams[k]):
+            mts[k].run(r_dev, streams[k].cuda_stream)
+            plans[k].set_dates_device(per, mts[k].fbs.data_ptr(), mts[k].pi.data_ptr())
+            plans[k].solve_device(args, vars_[k].data_ptr())
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    for k, m in enumerate(mts):
+        m.status(streams[k].cuda_stream)
+        plans[k].solve_status()
+    v = vars_[(a.steps - 1) % nf].cpu().numpy()
+    return {"value": per * a.steps / el, "unit": "VaR-dates/s", "ms_per_step": el / a.steps * 1e3,
+            "stage": "returns in HBM -> device MSM filters + tables (cvq_msm_tables) -> solve",
+            "var_matches_resident_tables": bool(np.array_equal(v, vals))}
 
 
 def cpu_baseline(c, ipt, uvs, ggp, ptf_mean, gpu_var, a):

@@ -228,6 +228,42 @@ def msm_filter(returns_c, n_in: int, k: int, m0: float, sig: float, b: float, ga
     return out
 
 
+class MsmTables:
+    """Device-resident MSM forecast stage (cvq_msm_tables): every asset's rolling-window
+    Hamilton filters, the per-state collapse onto unique vols and the forecast
+    combinations, written straight into device buffers that a QuadraturePlan reads in
+    place (set_dates_device).  Replaces the host assembly of
+    msm_estimation.integration_params_retrieval (msm_estimation.py:123-418) in the
+    timed end-to-end path; buffers are torch tensors on `device`."""
+
+    def __init__(self, params, k: int, state_map, q: int, n_in: int, T: int, device: int = 0):
+        import torch
+        self.k, self.q, self.n_in, self.T = int(k), int(q), int(n_in), int(T)
+        self.params = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(-1, 4))
+        self.dim = self.params.shape[0]
+        self.state_map = np.ascontiguousarray(np.asarray(state_map, dtype=np.int32).reshape(self.dim, -1))
+        self.device = int(device)
+        n = C.c_int64()
+        N.check(N.lib().cvq_msm_tables_scratch(self.dim, self.k, self.n_in, self.T, C.byref(n)),
+                "cvq_msm_tables_scratch")
+        dev = torch.device("cuda", self.device)
+        self.scratch = torch.empty(int(n.value), dtype=torch.float64, device=dev)
+        self.fbs = torch.empty((self.T, self.dim, self.q), dtype=torch.float64, device=dev)
+        self.pi = torch.empty((self.T, self.q ** self.dim), dtype=torch.float64, device=dev)
+
+    def run(self, returns_c_dev, stream: Optional[int] = None) -> None:
+        """returns_c_dev: device tensor [dim][n_in + T - 1] of centred returns (C-contiguous)."""
+        N.check(N.lib().cvq_msm_tables(self.device, C.c_void_p(stream or 0), self.dim, self.k, N.ptr(self.params),
+                                       self.state_map.ctypes.data_as(C.c_void_p), self.q,
+                                       C.c_void_p(returns_c_dev.data_ptr()), self.n_in, self.T,
+                                       C.c_void_p(self.scratch.data_ptr()), C.c_void_p(self.fbs.data_ptr()),
+                                       C.c_void_p(self.pi.data_ptr())), "cvq_msm_tables")
+
+    def status(self, stream: Optional[int] = None) -> None:
+        N.check(N.lib().cvq_msm_tables_status(C.c_void_p(self.scratch.data_ptr()), self.dim, self.k, self.n_in,
+                                              self.T, C.c_void_p(stream or 0)), "cvq_msm_tables_status")
+
+
 def garch_forecast(returns_c, n_in: int, omega: float, alpha: float, beta: float, device: int = 0) -> np.ndarray:
     r = N.f64(returns_c)
     T = r.size - n_in + 1

@@ -55,6 +55,18 @@ def msm_vol_states(k: int, m0: float, sig: float) -> np.ndarray:
     return np.array([np.sqrt(np.prod(M[i])) * sig for i in range(M.shape[0])])
 
 
+def unique_vol_map(vol_state_array: np.ndarray, tol: float = 1e-6):
+    """The state -> unique-vol index map of sum_forecast_by_state (msm_estimation.py:228-235):
+    (state_map (dim, S) int32, unique_vol_states (dim, q))."""
+    maps, uniq = [], []
+    for i in range(vol_state_array.shape[0]):
+        rounded = np.round(vol_state_array[i, :] / tol) * tol
+        u, inv = np.unique(rounded, return_inverse=True)
+        maps.append(inv.astype(np.int32))
+        uniq.append(u)
+    return np.array(maps), np.array(uniq)
+
+
 def sum_forecast_by_state(vol_state_array: np.ndarray, filtered: np.ndarray, tol: float = 1e-6):
     """msm_estimation.py:205-248: collapse states with equal (1e-6-rounded) vol (Q14).
     filtered (dim, T, S) -> forecasts_by_states (T, dim, q), unique_vol_states (dim, q)."""

@@ -32,6 +32,10 @@ struct MsmParams {
     double vs[128];    // vol states sqrt(prod M_s) * sigma (calc_prob.py:103-108)
 };
 
+struct MsmParamsN {
+    MsmParams a[3];                                // per asset (dim <= 3), passed by value
+};
+
 MsmParams msm_params(int k, double m0, double sigma, double b, double gamma) {
     MsmParams P{};
     for (int c = 0; c < k; ++c) {
@@ -54,6 +58,17 @@ MsmParams msm_params(int k, double m0, double sigma, double b, double gamma) {
 __device__ __forceinline__ double cond_prob(double r, double vs) {
     const double z = r / vs;
     return (1 / (vs * 2.5066282746310002)) * exp(-0.5 * (z * z));   // calc_prob.py:116-117
+}
+
+// Quad-local lane exchange of a double by DPP (xor 1: quad_perm [1,0,3,2]; xor 2:
+// [2,3,0,1]): a VALU move with no LDS round trip, unlike __shfl_xor's ds_bpermute --
+// the filter's per-step chain is latency-bound, so this sets its speed.
+template <int M>
+__device__ __forceinline__ double quad_xor(double v) {
+    constexpr int ctrl = M == 1 ? 0xB1 : 0x4E;
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
 
 template <int K>
@@ -85,7 +100,7 @@ __device__ __forceinline__ double msm_step(double (&v)[Quad<K>::SL], const doubl
             const int m = 1 << (pos - LB);
 #pragma unroll
             for (int j = 0; j < SL; ++j) {
-                const double o = __shfl_xor(v[j], m, 64);
+                const double o = m == 1 ? quad_xor<1>(v[j]) : quad_xor<2>(v[j]);
                 v[j] = pc * v[j] + qc * o;
             }
         }
@@ -97,26 +112,43 @@ __device__ __forceinline__ double msm_step(double (&v)[Quad<K>::SL], const doubl
         part += v[j];
     }
     double tot = part;
-    if (L >= 2) tot += __shfl_xor(tot, 1, 64);
-    if (L >= 4) tot += __shfl_xor(tot, 2, 64);
+    if (L >= 2) tot += quad_xor<1>(tot);
+    if (L >= 4) tot += quad_xor<2>(tot);
     *zero = !(tot != 0.0);
+    // 1 / tot: hardware reciprocal + two Newton steps (~1 ulp; the reference's v / tot
+    // rounds differently by ~1e-16, far below the 1e-8 node noise the VaR tolerates)
+    double inv = __builtin_amdgcn_rcp(tot);
+    inv = fma(inv, fma(-tot, inv, 1.0), inv);
+    inv = fma(inv, fma(-tot, inv, 1.0), inv);
 #pragma unroll
-    for (int j = 0; j < SL; ++j) v[j] = v[j] / tot;
+    for (int j = 0; j < SL; ++j) v[j] = v[j] * inv;
     return tot;
 }
 
-// cond[i][s] for every return of the series (shared by all windows containing i).
-__global__ void k_msm_cond(MsmParams P, int S, const double* __restrict__ r, long long N, double* __restrict__ cond) {
+// cond[d][i][s] for every return of each asset's series (shared by all windows containing i);
+// blockIdx.y = asset, its returns at r + d * N.
+__global__ void k_msm_cond(MsmParamsN PN, int S, const double* __restrict__ r, long long N, double* __restrict__ cond) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= N * S) return;
-    cond[idx] = cond_prob(r[idx / S], P.vs[idx % S]);
+    const int d = blockIdx.y;
+    cond[d * N * S + idx] = cond_prob(r[d * N + idx / S], PN.a[d].vs[idx % S]);
 }
 
-// Filtered state probabilities at the end of each window (calc_forecasts).
+// Filtered state probabilities at the end of each window (calc_forecasts), every asset
+// of the batch in one launch (blockIdx.y = asset; cond / out strides per asset).  The
+// window's N_in steps are a dependent chain, so the conditional densities of the next
+// kPrefetch steps are loaded ahead in a register ring: the chain waits on the FP64
+// math, not on an L2 round trip per step.
+constexpr int kPrefetch = 8;
+
 template <int K>
-__global__ __launch_bounds__(256) void k_msm_filter(MsmParams P, const double* __restrict__ cond, long long n_in,
-                                                    long long T, double* __restrict__ out, int* err) {
+__global__ __launch_bounds__(256) void k_msm_filter(MsmParamsN PN, const double* __restrict__ cond, long long cstride,
+                                                    long long n_in, long long T, double* __restrict__ out,
+                                                    long long ostride, int* err) {
     constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    const MsmParams& P = PN.a[blockIdx.y];
+    cond += blockIdx.y * cstride;
+    out += blockIdx.y * ostride;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long t = gid / L;
     const int lane_q = (int)(gid % L);
@@ -126,19 +158,64 @@ __global__ __launch_bounds__(256) void k_msm_filter(MsmParams P, const double* _
 #pragma unroll
     for (int j = 0; j < SL; ++j) v[j] = 1.0 / S;               // equi_prob (calc_prob.py:12-13)
     bool bad = false;
-    for (long long i = 0; i < n_in; ++i) {
-        double cv[SL];
-        const double* row = cond + (tt + i) * S + lane_q * SL;
+    const double* base = cond + tt * S + lane_q * SL;          // row i of this window: base + i * S
+    double ring[kPrefetch][SL];
 #pragma unroll
-        for (int j = 0; j < SL; ++j) cv[j] = row[j];
-        bool z;
-        msm_step<K>(v, cv, P, &z);
-        bad |= z;
+    for (int d = 0; d < kPrefetch; ++d)
+#pragma unroll
+        for (int j = 0; j < SL; ++j) ring[d][j] = d < n_in ? base[(long long)d * S + j] : 0.0;
+    for (long long i0 = 0; i0 < n_in; i0 += kPrefetch) {
+#pragma unroll
+        for (int d = 0; d < kPrefetch; ++d) {
+            const long long i = i0 + d;
+            if (i < n_in) {
+                double cv[SL];
+#pragma unroll
+                for (int j = 0; j < SL; ++j) cv[j] = ring[d][j];
+                const long long nx = i + kPrefetch;
+#pragma unroll
+                for (int j = 0; j < SL; ++j) ring[d][j] = nx < n_in ? base[nx * S + j] : 0.0;
+                bool z;
+                msm_step<K>(v, cv, P, &z);
+                bad |= z;
+            }
+        }
     }
     if (!active) return;
     if (bad) atomicOr(err, 1);
 #pragma unroll
     for (int j = 0; j < SL; ++j) out[t * S + lane_q * SL + j] = v[j];
+}
+
+// sum_forecast_by_state (msm_estimation.py:205-248, Q14) + compute_forecast_combinations
+// (:392-418, Q7) on the device: one thread per date t.  filt [dim][T][S] -> fbs [T][dim][q]
+// (states collapsed onto their unique 1e-6-rounded vol, summed in state order) and
+// pi [T][q^dim] in the reference's xy-meshgrid product order (2-D: f0[a] f1[b];
+// 3-D: (f0[L1] f1[L2]) f2[L0]).
+struct StateMap {
+    uint8_t u[3][128];                             // unique-vol index of state s of asset d
+};
+
+__global__ void k_msm_tables(StateMap M, int dim, int S, int q, const double* __restrict__ filt, long long T,
+                             double* __restrict__ fbs, double* __restrict__ pi) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    double f[3][8];
+    for (int d = 0; d < dim; ++d) {
+        for (int u = 0; u < q; ++u) f[d][u] = 0.0;
+        const double* row = filt + ((long long)d * T + t) * S;
+        for (int s2 = 0; s2 < S; ++s2) f[d][M.u[d][s2]] += row[s2];
+        for (int u = 0; u < q; ++u) fbs[(t * dim + d) * q + u] = f[d][u];
+    }
+    double* pt = pi + t * (dim == 2 ? q * q : q * q * q);
+    if (dim == 2) {
+        for (int a = 0; a < q; ++a)
+            for (int b = 0; b < q; ++b) pt[a * q + b] = f[0][a] * f[1][b];
+    } else {
+        for (int L0 = 0; L0 < q; ++L0)
+            for (int L1 = 0; L1 < q; ++L1)
+                for (int L2 = 0; L2 < q; ++L2) pt[(L0 * q + L1) * q + L2] = (f[0][L1] * f[1][L2]) * f[2][L0];
+    }
 }
 
 // Batched MSM log-likelihood (calc_prob.py:134-142 -> :36-47): one quad per candidate.
@@ -459,11 +536,27 @@ struct DevInt {
 };
 
 template <int K>
-void launch_filter(const MsmParams& P, const double* cond, long long n_in, long long T, double* out, int* err) {
+void launch_filter(const MsmParamsN& P, int dim, const double* cond, long long N, long long n_in, long long T,
+                   double* out, int* err, hipStream_t stream) {
     constexpr int L = Quad<K>::L;
     const long long threads = T * L;
-    hipLaunchKernelGGL(k_msm_filter<K>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, P, cond, n_in, T,
-                       out, err);
+    hipLaunchKernelGGL(k_msm_filter<K>, dim3((unsigned)((threads + 255) / 256), (unsigned)dim), dim3(256), 0, stream,
+                       P, cond, N * (1LL << K), n_in, T, out, T * (1LL << K), err);
+}
+
+int launch_filter_k(int k, const MsmParamsN& P, int dim, const double* cond, long long N, long long n_in, long long T,
+                    double* out, int* err, hipStream_t stream) {
+    switch (k) {
+        case 1: launch_filter<1>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        case 2: launch_filter<2>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        case 3: launch_filter<3>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        case 4: launch_filter<4>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        case 5: launch_filter<5>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        case 6: launch_filter<6>(P, dim, cond, N, n_in, T, out, err, stream); break;
+        default: launch_filter<7>(P, dim, cond, N, n_in, T, out, err, stream); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
 }
 
 template <int K>
@@ -485,6 +578,61 @@ int check_device(int device) {
 
 extern "C" {
 
+int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, int64_t* doubles) {
+    CVQ_REQUIRE(doubles != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(dim >= 1 && dim <= 3 && k >= 1 && k <= 7 && n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "bad shape");
+    const long long S = 1LL << k, N = n_in + T - 1;
+    *doubles = dim * N * S + dim * T * S + 2;     // cond, filtered probabilities, error word
+    return CVQ_OK;
+}
+
+int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, const double* params,
+                       const int32_t* state_map, int32_t q, const double* returns_c, int64_t n_in, int64_t T,
+                       double* scratch, double* fbs_out, double* pi_out) {
+    CVQ_REQUIRE(params && state_map && returns_c && scratch && fbs_out && pi_out, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(dim >= 2 && dim <= 3, CVQ_ERR_UNSUPPORTED, "dim must be 2 or 3");
+    CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
+    CVQ_REQUIRE(q >= 1 && q <= 8, CVQ_ERR_UNSUPPORTED, "q (unique vol states) must be in [1, 8]");
+    CVQ_REQUIRE(n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "n_in and T must be >= 1");
+    const int S = 1 << k;
+    MsmParamsN P{};
+    StateMap M{};
+    for (int d = 0; d < dim; ++d) {
+        P.a[d] = msm_params(k, params[4 * d], params[4 * d + 1], params[4 * d + 2], params[4 * d + 3]);
+        for (int s2 = 0; s2 < S; ++s2) {
+            CVQ_REQUIRE(state_map[d * S + s2] >= 0 && state_map[d * S + s2] < q, CVQ_ERR_INVALID,
+                        "state_map entries must be in [0, q)");
+            M.u[d][s2] = (uint8_t)state_map[d * S + s2];
+        }
+    }
+    int rc = check_device(device);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const long long N = n_in + T - 1;
+    double* cond = scratch;
+    double* filt = cond + (long long)dim * N * S;
+    int* err = (int*)(filt + (long long)dim * T * S);
+    CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,
+                       returns_c, N, cond);
+    if ((rc = launch_filter_k(k, P, dim, cond, N, n_in, T, filt, err, st))) return rc;
+    hipLaunchKernelGGL(k_msm_tables, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, M, dim, S, q, filt, T,
+                       fbs_out, pi_out);
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n_in, int64_t T, void* stream) {
+    CVQ_REQUIRE(scratch != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    const long long S = 1LL << k, N = n_in + T - 1;
+    int e = 0;
+    CVQ_HIP_CHECK(hipMemcpyAsync(&e, scratch + dim * N * S + dim * T * S, sizeof(int), hipMemcpyDeviceToHost,
+                                 (hipStream_t)stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");
+    return CVQ_OK;
+}
+
 int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
                        const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem) {
     CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
@@ -492,7 +640,8 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
     CVQ_REQUIRE(n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "n_in and T must be >= 1");
     int rc = check_device(device);
     if (rc) return rc;
-    const MsmParams P = msm_params(k, m0, sigma, b, gamma);
+    MsmParamsN P{};
+    P.a[0] = msm_params(k, m0, sigma, b, gamma);
     const int S = 1 << k;
     const long long N = n_in + T - 1;
     DevBuf rin, cond, dout;
@@ -504,16 +653,8 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
     CVQ_HIP_CHECK(hipMalloc((void**)&cond.p, (size_t)N * S * sizeof(double)));
     CVQ_HIP_CHECK(hipMalloc((void**)&err.p, sizeof(int)));
     CVQ_HIP_CHECK(hipMemset(err.p, 0, sizeof(int)));
-    hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256)), dim3(256), 0, 0, P, S, d_r, N, cond.p);
-    switch (k) {
-        case 1: launch_filter<1>(P, cond.p, n_in, T, d_out, err.p); break;
-        case 2: launch_filter<2>(P, cond.p, n_in, T, d_out, err.p); break;
-        case 3: launch_filter<3>(P, cond.p, n_in, T, d_out, err.p); break;
-        case 4: launch_filter<4>(P, cond.p, n_in, T, d_out, err.p); break;
-        case 5: launch_filter<5>(P, cond.p, n_in, T, d_out, err.p); break;
-        case 6: launch_filter<6>(P, cond.p, n_in, T, d_out, err.p); break;
-        default: launch_filter<7>(P, cond.p, n_in, T, d_out, err.p); break;
-    }
+    hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), 1), dim3(256), 0, 0, P, S, d_r, N, cond.p);
+    if ((rc = launch_filter_k(k, P, 1, cond.p, N, n_in, T, d_out, err.p, 0))) return rc;
     if ((rc = finish_out(out, (size_t)T * S, mem, dout))) return rc;
     int e = 0;
     CVQ_HIP_CHECK(hipMemcpy(&e, err.p, sizeof(int), hipMemcpyDeviceToHost));

@@ -172,6 +172,22 @@ int32_t cvq_solve_finalize_packed(cvq_plan* plan, const cvq_solve_args* args, co
  * window.  returns_c: centred returns [n_in + T - 1] of ONE asset; out [T][2**k]. */
 int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
                        const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
+/* Device-resident MSM forecast stage for all assets in one pass (no host round trip):
+ * forecasts_array (msm_estimation.py:140-202 -> calc_prob.py:8-69, filtered
+ * probabilities at each window's end, Q12) + sum_forecast_by_state (:205-248, Q14)
+ * + compute_forecast_combinations (:392-418, Q7), i.e. integrations_params_t ready for
+ * cvq_set_dates(..., CVQ_MEM_DEVICE).  Stream-ordered on `stream` (NULL = null stream),
+ * no synchronisation.  params (host) [dim][4] = (m0, sigma, b, gamma); state_map (host)
+ * [dim][2**k] = index of state s's 1e-6-rounded vol among the asset's q unique vols;
+ * returns_c (device) [dim][n_in + T - 1] centred returns; scratch (device) of
+ * cvq_msm_tables_scratch doubles; fbs_out (device) [T][dim][q]; pi_out (device)
+ * [T][q**dim].  cvq_msm_tables_status synchronises and reports a zero Bayes
+ * normaliser (calc_prob.py:64-65) as CVQ_ERR_NUMERIC. */
+int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, int64_t* doubles);
+int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, const double* params,
+                       const int32_t* state_map, int32_t q, const double* returns_c, int64_t n_in,
+                       int64_t T, double* scratch, double* fbs_out, double* pi_out);
+int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n_in, int64_t T, void* stream);
 /* GARCH(1,1) compute_forecast (garch_estimation.py:190-231 -> garch/forecast.py:5-19).
  * out [T] = sigma forecast per window. */
 int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double beta,
