@@ -106,3 +106,34 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(N, "_lib", None)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         N.lib()
+
+
+def test_new_entry_points_validate_on_the_host():
+    """Packed finalize layout, solve status and the device MSM tables reject bad arguments
+    before any HIP call."""
+    from copula_var import _native as N
+    lib = N.lib()
+    a = N.CvqSolveArgs(0.05, -3.0, -3.5, -2.0, -7.5, 0.0, -100.0, 1e-6, 0.0)
+    ln, off = C.c_int64(), C.c_int64()
+    assert lib.cvq_packed_block_len(C.byref(a), 1000, C.byref(ln), C.byref(off)) == N.CVQ_OK
+    s = C.c_int32()
+    lib.cvq_snap_stride(C.byref(a), C.byref(s))
+    assert off.value >= 1000 * s.value and off.value % 2 == 0 and ln.value == off.value + 2
+    assert lib.cvq_packed_block_len(C.byref(a), 0, C.byref(ln), C.byref(off)) == N.CVQ_ERR_INVALID
+    assert lib.cvq_solve_finalize_packed(None, C.byref(a), None, 1, 1, 1, None) == N.CVQ_ERR_INVALID
+    n = C.c_int64()
+    assert lib.cvq_msm_tables_scratch(2, 4, 1135, 1000, C.byref(n)) == N.CVQ_OK
+    assert n.value == 2 * 2134 * 16 + 2 * 1000 * 16 + 2
+    assert lib.cvq_msm_tables_scratch(4, 4, 1135, 1000, C.byref(n)) == N.CVQ_ERR_INVALID
+    prm = np.array([0.45, 1.2, 3.0, 0.3, 0.5, 1.2, 3.0, 0.3])
+    smap = np.zeros(32, dtype=np.int32)
+    buf = np.zeros(8)
+    f = lambda dim, k, q, sm: lib.cvq_msm_tables(0, None, dim, k, N.ptr(prm), sm.ctypes.data_as(C.c_void_p), q,
+                                                 N.ptr(buf), 10, 5, N.ptr(buf), N.ptr(buf), N.ptr(buf))
+    assert f(1, 4, 5, smap) == N.CVQ_ERR_UNSUPPORTED                      # dim 1 is not a copula
+    assert f(2, 8, 5, smap) == N.CVQ_ERR_UNSUPPORTED                      # k > 7
+    bad = smap.copy()
+    bad[3] = 9
+    assert f(2, 4, 5, bad) == N.CVQ_ERR_INVALID                           # state map outside [0, q)
+    assert lib.cvq_last_error()
+
