@@ -57,7 +57,7 @@ def parse():
                     help="CPU sample size (0 = four per worker: ~15 s of joblib work on config 2)")
     ap.add_argument("--cpu-jobs", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=1,
-                    help="MSM, 1 GPU: also time end-to-end steps (device forecast tables + solve, from returns)")
+                    help="1 GPU: also time end-to-end steps (device forecast tables + solve, from returns)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="independent batches in flight (one plan + HIP stream each); 1 = one batch at a time")
     ap.add_argument("--time-all", type=int, default=0,
@@ -194,7 +194,7 @@ def main():
     kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items() if v[1]}
 
     e2e = None
-    if a.e2e and c.model == "msm" and world == 1:
+    if a.e2e and world == 1:
         e2e = end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev)
 
     cpu = None
@@ -246,23 +246,31 @@ def main():
 
 def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):
     """End-to-end steps: centred returns resident in HBM -> every asset's
-    rolling-window MSM filters, state collapse and forecast combinations on the device
-    (cvq_msm_tables) -> the solve reading those tables in place.  Same batches in flight;
-    the VaR must equal the main loop's (tables resident) bit for bit."""
+    rolling-window forecasts on the device -> the solve reading those tables in place.
+    MSM: Hamilton filters, state collapse and forecast combinations (cvq_msm_tables);
+    GARCH / UKF: sigma forecasts written as [T][dim] (cvq_sigma_tables).  Same batches in
+    flight; the VaR must equal the main loop's (tables resident) bit for bit."""
     import torch
     from copula_var import engine, tables
-    vsa = np.array([tables.msm_vol_states(c.k, p["m_0"], p["sig"]) for p in c.msm_params])
-    smap, uvs = tables.unique_vol_map(vsa)
-    prm = [[p["m_0"], p["sig"], p["b"], p["gamma"]] for p in c.msm_params]
     r_dev = torch.tensor(np.ascontiguousarray(block[:-1].T), dtype=torch.float64, device=dev)
     nf = len(plans)
-    mts = [engine.MsmTables(prm, c.k, smap, uvs.shape[1], c.n_in, per, dev.index or 0) for _ in range(nf)]
+    if c.model == "msm":
+        vsa = np.array([tables.msm_vol_states(c.k, p["m_0"], p["sig"]) for p in c.msm_params])
+        smap, uvs = tables.unique_vol_map(vsa)
+        prm = [[p["m_0"], p["sig"], p["b"], p["gamma"]] for p in c.msm_params]
+        mts = [engine.MsmTables(prm, c.k, smap, uvs.shape[1], c.n_in, per, dev.index or 0) for _ in range(nf)]
+        ptrs = lambda m: (m.fbs.data_ptr(), m.pi.data_ptr())
+        stage = "returns in HBM -> device MSM filters + tables (cvq_msm_tables) -> solve"
+    else:
+        mts = [engine.SigmaTables(c.model, c.model_params(), c.n_in, per, dev.index or 0) for _ in range(nf)]
+        ptrs = lambda m: (m.sig.data_ptr(), None)
+        stage = f"returns in HBM -> device {c.model} sigma forecasts (cvq_sigma_tables) -> solve"
 
     def step(i):
         k = i % nf
         with torch.cuda.stream(streams[k]):
             mts[k].run(r_dev, streams[k].cuda_stream)
-            plans[k].set_dates_device(per, mts[k].fbs.data_ptr(), mts[k].pi.data_ptr())
+            plans[k].set_dates_device(per, *ptrs(mts[k]))
             plans[k].solve_device(args, vars_[k].data_ptr())
 
     for i in range(a.warmup):
@@ -278,8 +286,7 @@ def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):
         plans[k].solve_status()
     v = vars_[(a.steps - 1) % nf].cpu().numpy()
     return {"value": per * a.steps / el, "unit": "VaR-dates/s", "ms_per_step": el / a.steps * 1e3,
-            "stage": "returns in HBM -> device MSM filters + tables (cvq_msm_tables) -> solve",
-            "var_matches_resident_tables": bool(np.array_equal(v, vals))}
+            "stage": stage, "var_matches_resident_tables": bool(np.array_equal(v, vals))}
 
 
 def cpu_baseline(c, ipt, uvs, ggp, ptf_mean, gpu_var, a):

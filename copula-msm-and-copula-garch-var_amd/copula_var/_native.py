@@ -88,6 +88,8 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_msm_tables_scratch": (i32, [i32, i32, i64, i64, C.POINTER(C.c_int64)]),
         "cvq_msm_tables": (i32, [i32, v, i32, i32, v, v, i32, v, i64, i64, v, v, v]),
         "cvq_msm_tables_status": (i32, [v, i32, i32, i64, i64, v]),
+        "cvq_sigma_tables": (i32, [i32, v, i32, i32, v, v, v, i64, i64, v, v]),
+        "cvq_sigma_tables_status": (i32, [v, v]),
         "cvq_garch_forecast": (i32, [i32, d, d, d, v, i64, i64, v, i32]),
         "cvq_ukf_forecast": (i32, [i32, d, d, d, v, i64, i64, v, i32]),
         "cvq_garch_forecast_pq": (i32, [i32, i32, i32, v, v, i64, i64, v, i32]),

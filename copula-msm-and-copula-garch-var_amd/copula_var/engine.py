@@ -264,6 +264,58 @@ class MsmTables:
                                               self.T, C.c_void_p(stream or 0)), "cvq_msm_tables_status")
 
 
+class SigmaTables:
+    """Device-resident GARCH / UKF forecast stage (cvq_sigma_tables): every asset's
+    rolling-window sigma forecast written straight into a device [T][dim] buffer that a
+    QuadraturePlan reads in place (set_dates_device).  Replaces the host assembly of
+    Garch/MeanRevertingEstimation.integration_params_retrieval (garch_estimation.py:133-145,
+    mean_reverting_estimation.py:135-147) in the timed end-to-end path.
+
+    model 'garch': params = per-asset dicts {'omega','alpha','beta'} or {'pq': (p, q),
+    'params': (omega, alpha_1..p, beta_1..q)}; 'mean_reverting' (UKF): {'a','l','q'}."""
+
+    def __init__(self, model: str, params: Sequence[dict], n_in: int, T: int, device: int = 0):
+        import torch
+        self.n_in, self.T, self.device = int(n_in), int(T), int(device)
+        self.dim = len(params)
+        if model == "garch":
+            self.kind = N.GARCH
+            orders, flat = [], []
+            for p in params:
+                if "pq" in p:
+                    pq = (int(p["pq"][0]), int(p["pq"][1]))
+                    row = list(np.asarray(p["params"], dtype=np.float64).ravel())
+                    if len(row) != 1 + pq[0] + pq[1]:
+                        raise ValueError(f"GARCH{pq} needs {1 + sum(pq)} parameters, got {len(row)}")
+                else:
+                    pq, row = (1, 1), [p["omega"], p["alpha"], p["beta"]]
+                orders += pq
+                flat += row
+            self.orders = np.ascontiguousarray(orders, dtype=np.int32)
+        elif model in ("mean_reverting", "ukf"):
+            self.kind = N.UKF
+            self.orders = None
+            flat = [v for p in params for v in (p["a"], p["l"], p["q"])]
+        else:
+            raise ValueError(f"SigmaTables: model must be 'garch' or 'mean_reverting', got {model!r}")
+        self.params = np.ascontiguousarray(flat, dtype=np.float64)
+        dev = torch.device("cuda", self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.sig = torch.empty((self.T, self.dim), dtype=torch.float64, device=dev)
+
+    def run(self, returns_c_dev, stream: Optional[int] = None) -> None:
+        """returns_c_dev: device tensor [dim][n_in + T - 1] of centred returns (C-contiguous)."""
+        orders = self.orders.ctypes.data_as(C.c_void_p) if self.orders is not None else None
+        N.check(N.lib().cvq_sigma_tables(self.device, C.c_void_p(stream or 0), self.kind, self.dim, orders,
+                                         N.ptr(self.params), C.c_void_p(returns_c_dev.data_ptr()), self.n_in,
+                                         self.T, C.c_void_p(self.err.data_ptr()), C.c_void_p(self.sig.data_ptr())),
+                "cvq_sigma_tables")
+
+    def status(self, stream: Optional[int] = None) -> None:
+        N.check(N.lib().cvq_sigma_tables_status(C.c_void_p(self.err.data_ptr()), C.c_void_p(stream or 0)),
+                "cvq_sigma_tables_status")
+
+
 def garch_forecast(returns_c, n_in: int, omega: float, alpha: float, beta: float, device: int = 0) -> np.ndarray:
     r = N.f64(returns_c)
     T = r.size - n_in + 1

@@ -187,6 +187,187 @@ __global__ __launch_bounds__(256) void k_msm_filter(MsmParamsN PN, const double*
     for (int j = 0; j < SL; ++j) out[t * S + lane_q * SL + j] = v[j];
 }
 
+// ------------------------------------------------------- blocked (time-parallel) filter
+// The filter is linear up to its per-step normalisation: window t's filtered vector is
+// normalise(M_{t+n-1} ... M_t u), M_i = diag(c_i) A, u uniform (calc_prob.py:12-13,
+// :51-69).  Rolling windows share all but one of their steps, so the series is cut into
+// blocks of kBlk steps whose products G_b = M_{(b+1)B-1} ... M_{bB} are formed once
+// (k_msm_gblocks, every block in parallel); window t then runs only its partial first and
+// last blocks as filter steps and crosses the full blocks in between with one dense
+// G_b mat-vec each (k_msm_windows): <= 2B + n/B dependent steps instead of n.  All terms
+// are non-negative, so the reordering is benign (no cancellation): the forecasts agree
+// with the step-by-step filter to ~1e-14 relative.
+//
+// k_msm_gblocks: column j of G_b is the un-normalised filter run from e_j over the block;
+// every step is scaled by the common factor 1 / max_s c_i[s] (the same for all columns,
+// so it cancels on the final normalisation) to keep entries <= 1.  One quad per column.
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_gblocks(MsmParamsN PN, const double* __restrict__ cond,
+                                                     long long cstride, int B, int nfull, double* __restrict__ G,
+                                                     long long gstride, int* err) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    const MsmParams& P = PN.a[blockIdx.y];
+    cond += blockIdx.y * cstride;
+    G += blockIdx.y * gstride;
+    const int col = threadIdx.x / L, lane_q = threadIdx.x % L;
+    const int b = blockIdx.x;
+    if (b >= nfull || col >= S) return;
+    double v[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = (lane_q * SL + j == col) ? 1.0 : 0.0;
+    const double* base = cond + (long long)b * B * S + lane_q * SL;
+    bool bad = false;
+    for (int i = 0; i < B; ++i) {
+        double cv[SL], m = 0.0;
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            cv[j] = base[(long long)i * S + j];
+            m = fmax(m, cv[j]);
+        }
+        if (L >= 2) m = fmax(m, quad_xor<1>(m));
+        if (L >= 4) m = fmax(m, quad_xor<2>(m));
+        bad |= !(m > 0.0);                             // every state's density is 0: calc_prob.py:64-65
+        const double s = 1.0 / m;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const int pos = K - 1 - c;
+            const double pc = P.p[c], qc = P.qv[c];
+            if (pos < Quad<K>::LB) {
+                double nv[SL];
+#pragma unroll
+                for (int j = 0; j < SL; ++j) nv[j] = pc * v[j] + qc * v[j ^ (1 << pos)];
+#pragma unroll
+                for (int j = 0; j < SL; ++j) v[j] = nv[j];
+            } else {
+                const int mm = 1 << (pos - Quad<K>::LB);
+#pragma unroll
+                for (int j = 0; j < SL; ++j) {
+                    const double o = mm == 1 ? quad_xor<1>(v[j]) : quad_xor<2>(v[j]);
+                    v[j] = pc * v[j] + qc * o;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SL; ++j) v[j] = v[j] * (cv[j] * s);
+    }
+    if (bad && col == 0 && lane_q == 0) atomicOr(err, 1);
+    double* g = G + (long long)b * S * S;                       // G_b[r][c], row-major
+#pragma unroll
+    for (int j = 0; j < SL; ++j) g[(lane_q * SL + j) * S + col] = v[j];
+}
+
+// k_msm_windows: one quad per window, kWinPerWG windows per workgroup; the full blocks any
+// of the workgroup's windows crosses are staged in LDS once.
+constexpr int kWinPerWG = 16;
+
+template <int K>
+__device__ __forceinline__ void msm_steps(double (&v)[Quad<K>::SL], const double* __restrict__ base, long long i0,
+                                          long long i1, const MsmParams& P, bool* bad) {
+    constexpr int SL = Quad<K>::SL;
+    constexpr int S = Quad<K>::S;
+    constexpr int PF = 4;                                       // rows in flight ahead of the chain
+    double ring[PF][SL];
+#pragma unroll
+    for (int d = 0; d < PF; ++d)
+#pragma unroll
+        for (int j = 0; j < SL; ++j) ring[d][j] = (i0 + d < i1) ? base[(i0 + d) * S + j] : 0.0;
+    for (long long i = i0; i < i1; i += PF) {
+#pragma unroll
+        for (int d = 0; d < PF; ++d) {
+            if (i + d < i1) {
+                double cv[SL];
+#pragma unroll
+                for (int j = 0; j < SL; ++j) cv[j] = ring[d][j];
+                const long long nx = i + d + PF;
+#pragma unroll
+                for (int j = 0; j < SL; ++j) ring[d][j] = nx < i1 ? base[nx * S + j] : 0.0;
+                bool z;
+                msm_step<K>(v, cv, P, &z);
+                *bad |= z;
+            }
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void k_msm_windows(MsmParamsN PN, const double* __restrict__ cond, long long cstride,
+                                                    const double* __restrict__ G, long long gstride, int B,
+                                                    long long n_in, long long T, double* __restrict__ out,
+                                                    long long ostride, int* err) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    static_assert(L == 4 && SL * L == S, "blocked filter: a quad holds the states (2 <= k <= 4)");
+    extern __shared__ __attribute__((aligned(16))) double gl[];       // [nb][S][S]
+    const MsmParams& P = PN.a[blockIdx.y];
+    cond += blockIdx.y * cstride;
+    G += blockIdx.y * gstride;
+    out += blockIdx.y * ostride;
+    const long long t0 = (long long)blockIdx.x * kWinPerWG;
+    const long long tl = min(t0 + kWinPerWG, T) - 1;                  // last window of the workgroup
+    const long long blo = t0 / B + 1, bhi = (tl + n_in - 1) / B - 1;  // full blocks crossed by any window
+    const long long nb = bhi >= blo ? bhi - blo + 1 : 0;
+    {
+        const double2* src = (const double2*)(G + blo * S * S);
+        double2* dst = (double2*)gl;
+        for (long long w = threadIdx.x; w < nb * S * S / 2; w += blockDim.x) dst[w] = src[w];
+    }
+    __syncthreads();
+    const long long t = t0 + threadIdx.x / L;
+    const int lane_q = threadIdx.x % L;
+    const bool active = t < T;
+    const long long tt = active ? t : T - 1;
+    const long long b0 = tt / B, b1 = (tt + n_in - 1) / B;            // b1 >= b0 + 1 (host: n_in > B)
+    double v[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = 1.0 / S;                      // equi_prob (calc_prob.py:12-13)
+    bool bad = false;
+    const double* base = cond + lane_q * SL;
+    msm_steps<K>(v, base, tt, (b0 + 1) * B, P, &bad);                 // first partial block
+    for (long long b = b0 + 1; b < b1; ++b) {                         // full blocks: dense mat-vec
+        // the window's whole vector: src[x] = the states of quad lane lane_q ^ x
+        double src[4][SL];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            src[0][j] = v[j];
+            src[1][j] = quad_xor<1>(v[j]);
+            src[2][j] = quad_xor<2>(v[j]);
+            src[3][j] = quad_xor<1>(src[2][j]);
+        }
+        const double* g = gl + (b - blo) * S * S + lane_q * SL * S;   // this lane's SL rows
+        double part = 0.0;
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const double* gp = g + j * S + (lane_q ^ x) * SL;     // columns of lane lane_q ^ x
+                if constexpr (SL == 1) {
+                    a0 = fma(gp[0], src[x][0], a0);
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < SL; jj += 2) {
+                        const double2 gg = *(const double2*)(gp + jj);
+                        a0 = fma(gg.x, src[x][jj], a0);
+                        a1 = fma(gg.y, src[x][jj + 1], a1);
+                    }
+                }
+            }
+            v[j] = a0 + a1;
+            part += v[j];
+        }
+        double tot = part + quad_xor<1>(part);
+        tot += quad_xor<2>(tot);
+        bad |= !(tot > 0.0);
+        const double inv = 1.0 / tot;
+#pragma unroll
+        for (int j = 0; j < SL; ++j) v[j] *= inv;
+    }
+    msm_steps<K>(v, base, b1 * B, tt + n_in, P, &bad);                // last partial block
+    if (!active) return;
+    if (bad) atomicOr(err, 1);
+#pragma unroll
+    for (int j = 0; j < SL; ++j) out[t * S + lane_q * SL + j] = v[j];
+}
+
 // sum_forecast_by_state (msm_estimation.py:205-248, Q14) + compute_forecast_combinations
 // (:392-418, Q7) on the device: one thread per date t.  filt [dim][T][S] -> fbs [T][dim][q]
 // (states collapsed onto their unique 1e-6-rounded vol, summed in state order) and
@@ -366,6 +547,65 @@ __global__ void k_garch_forecast_pq(const double* __restrict__ prm, const double
     out[t0] = sqrt((omega + s_a) + s_b);
 }
 
+// Device-resident sigma stage (cvq_sigma_tables): the same recursion for one asset of a
+// batch, parameters by value, the forecast written straight into the solve's
+// integrations_params_t layout out[t * ostride] (ostride = dim).
+struct GarchPrm {
+    double v[1 + 2 * 4];
+};
+
+template <int P, int Q>
+__global__ void k_garch_sigma(GarchPrm G, const double* __restrict__ r, long long n_in, long long T,
+                              double* __restrict__ out, int ostride) {
+    const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 >= T) return;
+    const double* w = r + t0;
+    const double omega = G.v[0];
+    double alpha[P], beta[Q], sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) { alpha[i] = G.v[1 + i]; sa += alpha[i]; }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) { beta[j] = G.v[1 + P + j]; sb += beta[j]; }
+    double hist[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) hist[j] = 0.0;
+    hist[0] = omega / (1 - sa - sb);
+    for (long long t = 1; t < n_in; ++t) {
+        double v = omega;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (i < t) v += alpha[i] * (w[t - i - 1] * w[t - i - 1]);
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+            if (j < t) v += beta[j] * hist[j];
+        const double s2 = (v < 1e-7) ? 1e-7 : v;
+#pragma unroll
+        for (int j = Q - 1; j > 0; --j) hist[j] = hist[j - 1];
+        hist[0] = s2;
+    }
+    double s_a = 0.0, s_b = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const double ri = w[n_in - P + i];
+        s_a = (i == 0) ? alpha[i] * (ri * ri) : s_a + alpha[i] * (ri * ri);
+    }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) s_b = (j == 0) ? beta[j] * hist[Q - 1] : s_b + beta[j] * hist[Q - 1 - j];
+    out[t0 * ostride] = sqrt((omega + s_a) + s_b);
+}
+
+template <int P>
+void launch_garch_sigma(int q, const GarchPrm& G, const double* r, long long n_in, long long T, double* o, int os,
+                        hipStream_t st) {
+    const dim3 g((unsigned)((T + 255) / 256)), blk(256);
+    switch (q) {
+        case 1: hipLaunchKernelGGL((k_garch_sigma<P, 1>), g, blk, 0, st, G, r, n_in, T, o, os); break;
+        case 2: hipLaunchKernelGGL((k_garch_sigma<P, 2>), g, blk, 0, st, G, r, n_in, T, o, os); break;
+        case 3: hipLaunchKernelGGL((k_garch_sigma<P, 3>), g, blk, 0, st, G, r, n_in, T, o, os); break;
+        default: hipLaunchKernelGGL((k_garch_sigma<P, 4>), g, blk, 0, st, G, r, n_in, T, o, os); break;
+    }
+}
+
 template <int P>
 void launch_garch_forecast_pq(int q, const double* prm, const double* r, long long n_in, long long T, double* o) {
     const dim3 g((unsigned)((T + 255) / 256)), blk(256);
@@ -468,6 +708,26 @@ __global__ void k_ukf_forecast(UkfConst C, double a, double l, double q, const d
     out[t] = exp(xm);                                             // forecast.py:12 (Q19)
 }
 
+// cvq_sigma_tables' UKF leg: every asset in one launch (blockIdx.y = asset; its centred
+// returns at r + d * rstride), sigma written as out[t * dim + d].
+struct UkfPrmN {
+    double a[3], l[3], q[3];
+};
+
+__global__ void k_ukf_sigma(UkfConst C, UkfPrmN U, const double* __restrict__ r, long long rstride, long long n_in,
+                            long long T, double* __restrict__ out, int* err) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int d = blockIdx.y;
+    double xm, ll;
+    if (!ukf_pass(C, U.a[d], U.l[d], U.q[d], r + d * rstride + t, n_in, &xm, &ll)) {
+        atomicOr(err, 1);
+        out[t * gridDim.y + d] = __builtin_nan("");
+        return;
+    }
+    out[t * gridDim.y + d] = exp(xm);                             // forecast.py:12 (Q19)
+}
+
 __global__ void k_ukf_loglik(UkfConst C, const double* __restrict__ prm, long long B, const double* __restrict__ r,
                              long long N, double* __restrict__ out) {
     const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -559,6 +819,49 @@ int launch_filter_k(int k, const MsmParamsN& P, int dim, const double* cond, lon
     return CVQ_OK;
 }
 
+// Block length of the blocked filter for 2**k states and windows of n_in steps, or 0 for
+// the step-by-step filter (k outside [2, 4], windows not longer than a block, or the
+// full blocks a workgroup's windows cross would not fit kBlockLdsMax of LDS).
+constexpr size_t kBlockLdsMax = 80 * 1024;
+#ifndef CVQ_MSM_BLOCK
+#define CVQ_MSM_BLOCK 32
+#endif
+
+size_t blocked_lds_bytes(int k, long long n_in, int B) {
+    const long long S = 1LL << k;
+    return (size_t)((kWinPerWG - 1 + n_in - 1) / B + 1) * S * S * sizeof(double);
+}
+
+int msm_block_len(int k, long long n_in) {
+    if (k < 2 || k > 4 || CVQ_MSM_BLOCK <= 0) return 0;
+    int B = CVQ_MSM_BLOCK;
+    while (blocked_lds_bytes(k, n_in, B) > kBlockLdsMax) B *= 2;
+    return n_in > B ? B : 0;
+}
+
+template <int K>
+void launch_blocked(const MsmParamsN& P, int dim, const double* cond, long long N, long long n_in, long long T, int B,
+                    double* G, double* out, int* err, hipStream_t stream) {
+    constexpr int S = 1 << K;
+    const long long nfull = N / B;
+    hipLaunchKernelGGL(k_msm_gblocks<K>, dim3((unsigned)nfull, (unsigned)dim), dim3(4 * S), 0, stream, P, cond,
+                       N * S, B, (int)nfull, G, nfull * S * S, err);
+    hipLaunchKernelGGL(k_msm_windows<K>, dim3((unsigned)((T + kWinPerWG - 1) / kWinPerWG), (unsigned)dim),
+                       dim3(4 * kWinPerWG), blocked_lds_bytes(K, n_in, B), stream, P, cond, N * S, G, nfull * S * S,
+                       B, n_in, T, out, T * S, err);
+}
+
+int launch_blocked_k(int k, const MsmParamsN& P, int dim, const double* cond, long long N, long long n_in, long long T,
+                     int B, double* G, double* out, int* err, hipStream_t stream) {
+    switch (k) {
+        case 2: launch_blocked<2>(P, dim, cond, N, n_in, T, B, G, out, err, stream); break;
+        case 3: launch_blocked<3>(P, dim, cond, N, n_in, T, B, G, out, err, stream); break;
+        default: launch_blocked<4>(P, dim, cond, N, n_in, T, B, G, out, err, stream); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
 template <int K>
 void launch_msm_ll(const MsmParams* P, long long B, const double* r, long long N, double* out) {
     constexpr int L = Quad<K>::L;
@@ -582,7 +885,9 @@ int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, 
     CVQ_REQUIRE(doubles != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(dim >= 1 && dim <= 3 && k >= 1 && k <= 7 && n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "bad shape");
     const long long S = 1LL << k, N = n_in + T - 1;
-    *doubles = dim * N * S + dim * T * S + 2;     // cond, filtered probabilities, error word
+    const int B = msm_block_len(k, n_in);
+    const long long G = B ? dim * (N / B) * S * S : 0;      // blocked filter: full-block products
+    *doubles = dim * N * S + dim * T * S + G + 2;          // cond, filtered probabilities, [G], error word
     return CVQ_OK;
 }
 
@@ -609,13 +914,17 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const long long N = n_in + T - 1;
+    const int B = msm_block_len(k, n_in);
     double* cond = scratch;
     double* filt = cond + (long long)dim * N * S;
-    int* err = (int*)(filt + (long long)dim * T * S);
+    double* G = filt + (long long)dim * T * S;
+    int* err = (int*)(G + (B ? (long long)dim * (N / B) * S * S : 0));
     CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
     hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,
                        returns_c, N, cond);
-    if ((rc = launch_filter_k(k, P, dim, cond, N, n_in, T, filt, err, st))) return rc;
+    if (B) rc = launch_blocked_k(k, P, dim, cond, N, n_in, T, B, G, filt, err, st);
+    else rc = launch_filter_k(k, P, dim, cond, N, n_in, T, filt, err, st);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_msm_tables, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, M, dim, S, q, filt, T,
                        fbs_out, pi_out);
     CVQ_HIP_CHECK(hipGetLastError());
@@ -625,11 +934,78 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
 int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n_in, int64_t T, void* stream) {
     CVQ_REQUIRE(scratch != nullptr, CVQ_ERR_INVALID, "NULL argument");
     const long long S = 1LL << k, N = n_in + T - 1;
+    const int B = msm_block_len(k, n_in);
+    const long long G = B ? dim * (N / B) * S * S : 0;
     int e = 0;
-    CVQ_HIP_CHECK(hipMemcpyAsync(&e, scratch + dim * N * S + dim * T * S, sizeof(int), hipMemcpyDeviceToHost,
+    CVQ_HIP_CHECK(hipMemcpyAsync(&e, scratch + dim * N * S + dim * T * S + G, sizeof(int), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));
     CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
     CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");
+    return CVQ_OK;
+}
+
+int32_t cvq_sigma_tables(int32_t device, void* stream, int32_t model, int32_t dim, const int32_t* orders,
+                         const double* params, const double* returns_c, int64_t n_in, int64_t T, int32_t* d_err,
+                         double* sig_out) {
+    CVQ_REQUIRE(params && returns_c && d_err && sig_out, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(model == CVQ_GARCH || model == CVQ_UKF, CVQ_ERR_UNSUPPORTED, "model must be CVQ_GARCH or CVQ_UKF");
+    CVQ_REQUIRE(dim >= 2 && dim <= 3, CVQ_ERR_UNSUPPORTED, "dim must be 2 or 3");
+    CVQ_REQUIRE(n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "n_in and T must be >= 1");
+    GarchPrm G[3]{};
+    int po[3] = {1, 1, 1}, qo[3] = {1, 1, 1};
+    UkfPrmN U{};
+    const double* pp = params;
+    for (int d = 0; d < dim; ++d) {
+        if (model == CVQ_GARCH) {
+            if (orders) { po[d] = orders[2 * d]; qo[d] = orders[2 * d + 1]; }
+            CVQ_REQUIRE(po[d] >= 1 && qo[d] >= 1 && po[d] <= kGarchMaxPQ && qo[d] <= kGarchMaxPQ, CVQ_ERR_UNSUPPORTED,
+                        "GARCH orders must be 1 <= p, q <= 4");
+            CVQ_REQUIRE(n_in >= po[d] && n_in >= qo[d], CVQ_ERR_INVALID, "window shorter than the GARCH order");
+            double s = 0.0;
+            bool pos = pp[0] > 0;
+            for (int i = 0; i < 1 + po[d] + qo[d]; ++i) {
+                G[d].v[i] = pp[i];
+                if (i) { pos = pos && pp[i] > 0; s += pp[i]; }
+            }
+            CVQ_REQUIRE(pos && s < 1, CVQ_ERR_INVALID,
+                        "GARCH parameters must be positive with sum(alpha) + sum(beta) < 1 (garch/estimation.py:22-38)");
+            pp += 1 + po[d] + qo[d];
+        } else {
+            U.a[d] = pp[0];
+            U.l[d] = pp[1];
+            U.q[d] = pp[2];
+            pp += 3;
+        }
+    }
+    int rc = check_device(device);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const long long N = n_in + T - 1;
+    CVQ_HIP_CHECK(hipMemsetAsync(d_err, 0, sizeof(int32_t), st));
+    if (model == CVQ_GARCH) {
+        for (int d = 0; d < dim; ++d) {
+            const double* r = returns_c + d * N;
+            switch (po[d]) {
+                case 1: launch_garch_sigma<1>(qo[d], G[d], r, n_in, T, sig_out + d, dim, st); break;
+                case 2: launch_garch_sigma<2>(qo[d], G[d], r, n_in, T, sig_out + d, dim, st); break;
+                case 3: launch_garch_sigma<3>(qo[d], G[d], r, n_in, T, sig_out + d, dim, st); break;
+                default: launch_garch_sigma<4>(qo[d], G[d], r, n_in, T, sig_out + d, dim, st); break;
+            }
+        }
+    } else {
+        hipLaunchKernelGGL(k_ukf_sigma, dim3((unsigned)((T + 63) / 64), (unsigned)dim), dim3(64), 0, st, ukf_const(), U,
+                           returns_c, N, n_in, T, sig_out, (int*)d_err);
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
+int32_t cvq_sigma_tables_status(const int32_t* d_err, void* stream) {
+    CVQ_REQUIRE(d_err != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    int e = 0;
+    CVQ_HIP_CHECK(hipMemcpyAsync(&e, d_err, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "UKF normaliser Z < 1e-10 (estimate.py:219-220; reference returns None)");
     return CVQ_OK;
 }
 

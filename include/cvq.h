@@ -201,6 +201,23 @@ int32_t cvq_garch_forecast_pq(int32_t device, int32_t p, int32_t q, const double
 int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q,
                          const double* returns_c, int64_t n_in, int64_t T, double* out, int32_t mem);
 
+/* Device-resident GARCH / UKF forecast stage for all assets (no host round trip):
+ * Garch/MeanRevertingEstimation.integration_params_retrieval's sigma forecasts
+ * (garch_estimation.py:133-145 -> :190-231 -> garch/forecast.py:5-19;
+ * mean_reverting_estimation.py:135-147 -> :192-232 -> kalman_mean_reverting/forecast.py:5-12),
+ * written as integrations_params_t [T][dim] for cvq_set_dates(..., CVQ_MEM_DEVICE).
+ * Stream-ordered on `stream`, no synchronisation.  model CVQ_GARCH: orders (host)
+ * [dim][2] = (p, q) per asset, 1 <= p, q <= 4 (NULL = all (1, 1)), params (host) the
+ * assets' (omega, alpha_1..p, beta_1..q) rows back to back; CVQ_UKF: params (host)
+ * [dim][3] = (a, l, q), orders ignored.  returns_c (device) [dim][n_in + T - 1];
+ * d_err (device) one int32; sig_out (device) [T][dim].  cvq_sigma_tables_status
+ * synchronises and reports a UKF failure (Z < 1e-10 / NaN, estimate.py:219-220,
+ * :270-271; NaN sigma) as CVQ_ERR_NUMERIC. */
+int32_t cvq_sigma_tables(int32_t device, void* stream, int32_t model, int32_t dim, const int32_t* orders,
+                         const double* params, const double* returns_c, int64_t n_in, int64_t T,
+                         int32_t* d_err, double* sig_out);
+int32_t cvq_sigma_tables_status(const int32_t* d_err, void* stream);
+
 /* --------------------------------------- batched in-sample likelihoods */
 /* One log-likelihood per parameter candidate over the same return series
  * (optimiser inner loops).  params: MSM [B][4] = (m0, sigma, b, gamma);

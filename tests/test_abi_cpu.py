@@ -123,7 +123,7 @@ def test_new_entry_points_validate_on_the_host():
     assert lib.cvq_solve_finalize_packed(None, C.byref(a), None, 1, 1, 1, None) == N.CVQ_ERR_INVALID
     n = C.c_int64()
     assert lib.cvq_msm_tables_scratch(2, 4, 1135, 1000, C.byref(n)) == N.CVQ_OK
-    assert n.value == 2 * 2134 * 16 + 2 * 1000 * 16 + 2
+    assert n.value == 2 * 2134 * 16 + 2 * 1000 * 16 + 2 * (2134 // 32) * 16 * 16 + 2   # cond, filt, G blocks, err
     assert lib.cvq_msm_tables_scratch(4, 4, 1135, 1000, C.byref(n)) == N.CVQ_ERR_INVALID
     prm = np.array([0.45, 1.2, 3.0, 0.3, 0.5, 1.2, 3.0, 0.3])
     smap = np.zeros(32, dtype=np.int32)
@@ -137,3 +137,27 @@ def test_new_entry_points_validate_on_the_host():
     assert f(2, 4, 5, bad) == N.CVQ_ERR_INVALID                           # state map outside [0, q)
     assert lib.cvq_last_error()
 
+
+
+def test_sigma_tables_validate_on_the_host():
+    """cvq_sigma_tables (device GARCH / UKF forecast stage) rejects bad arguments before any
+    HIP call."""
+    from copula_var import _native as N
+    lib = N.lib()
+    buf = np.zeros(16)
+    err = np.zeros(1, dtype=np.int32)
+    ok_orders = np.array([1, 1, 2, 1], dtype=np.int32)
+    garch = np.array([0.05, 0.08, 0.90, 0.05, 0.04, 0.04, 0.90])
+    f = lambda model, dim, orders, prm: lib.cvq_sigma_tables(
+        0, None, model, dim, orders.ctypes.data_as(C.c_void_p) if orders is not None else None, N.ptr(prm),
+        N.ptr(buf), 10, 5, err.ctypes.data_as(C.c_void_p), N.ptr(buf))
+    assert f(N.MSM, 2, None, garch) == N.CVQ_ERR_UNSUPPORTED               # MSM has cvq_msm_tables
+    assert f(N.GARCH, 1, None, garch) == N.CVQ_ERR_UNSUPPORTED             # dim 1
+    assert f(N.GARCH, 2, np.array([1, 5, 1, 1], dtype=np.int32), garch) == N.CVQ_ERR_UNSUPPORTED   # q > 4
+    nonstat = garch.copy()
+    nonstat[6] = 0.95                                                      # alpha_1 + alpha_2 + beta >= 1
+    assert f(N.GARCH, 2, ok_orders, nonstat) == N.CVQ_ERR_INVALID
+    assert lib.cvq_sigma_tables(0, None, N.UKF, 2, None, None, N.ptr(buf), 10, 5,
+                                err.ctypes.data_as(C.c_void_p), N.ptr(buf)) == N.CVQ_ERR_INVALID
+    assert lib.cvq_sigma_tables_status(None, None) == N.CVQ_ERR_INVALID
+    assert lib.cvq_last_error()
