@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
-    ap.add_argument("--strategy", default="auto", choices=["auto", "prefix", "direct", "compact", "sorted"],
+    ap.add_argument("--strategy", default="auto", choices=["auto", "prefix", "direct", "compact", "sorted", "sweep"],
                     help="auto: COMPACT for 2-asset MSM, SORTED otherwise (engine.auto_strategy)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
     ap.add_argument("--cpu-dates", type=int, default=0,
@@ -224,7 +224,8 @@ def main():
                          "kernel": {"prefix": "k_mass (joint-mass row prefix)",
                                     "direct": "k_direct (per-date slab-on-the-fly solve)",
                                     "compact": "k_compact (per-date solve, one-wave tail)",
-                                    "sorted": "k_sorted (per-date solve over the v*-sorted node list)"}[a.strategy],
+                                    "sorted": "k_sorted (per-date solve over the v*-sorted node list)",
+                                    "sweep": "k_sorted<SWEEP> (per-date solve, one pass per bisection cell)"}[a.strategy],
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_us": dom_avg_s * 1e6,
                          "achieved_per_step": achieved_step,
                          "reach_nodes_per_date": plan.reach_nodes,

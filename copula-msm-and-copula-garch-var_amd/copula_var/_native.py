@@ -28,7 +28,7 @@ CVQ_ERR_NUMERIC = -7
 MEM_HOST, MEM_DEVICE = 0, 1
 GAUSSIAN, STUDENT, PLACKETT = 0, 1, 2
 MSM, GARCH, UKF = 0, 1, 2
-STRATEGY_PREFIX, STRATEGY_DIRECT, STRATEGY_COMPACT, STRATEGY_SORTED = 0, 1, 2, 3
+STRATEGY_PREFIX, STRATEGY_DIRECT, STRATEGY_COMPACT, STRATEGY_SORTED, STRATEGY_SWEEP = 0, 1, 2, 3, 4
 
 COPULA_KIND = {"gaussian": GAUSSIAN, "student": STUDENT, "plackett": PLACKETT}
 MODEL_KIND = {"msm": MSM, "garch": GARCH, "mean_reverting": UKF, "ukf": UKF}

@@ -71,7 +71,8 @@ class QuadraturePlan:
         if strategy == "auto":
             strategy = auto_strategy(model, self.dim)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
-                       "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED}[strategy]
+                       "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED,
+                       "sweep": N.STRATEGY_SWEEP}[strategy]
         self.strategy = strategy
         st.v_cap = float(v_cap)
         self._static = st

@@ -162,6 +162,12 @@ struct cvq_plan {
     double* d_svs = nullptr;     // [G]
     int* d_tree = nullptr;       // [4][1 << tree_depth]
     int tree_depth = 0;
+    int* d_sweep0 = nullptr;     // SWEEP: pass-0 boundary list
+    uint32_t* d_trw0 = nullptr;  // SWEEP: transposed node words of pass 0 / bracket 2's root pass
+    uint32_t* d_trw2 = nullptr;
+    std::vector<uint32_t> hidx;  // SORTED node words (host copy, SWEEP transposes ranges of it)
+    int sweep_d0 = 0, sweep_d = 0;
+    bool sweep_ok = false;       // SWEEP usable for the cached solve arguments (levels ordered)
     int fixpos[6] = {0, 0, 0, 0, 0, 0};
     double tree_key[7] = {0, 0, 0, 0, 0, 0, 0};
     bool tree_valid = false;
@@ -469,6 +475,53 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
     p->tree_valid = false;
     if (int rc = dev_alloc(&p->d_tree, tree.size())) return rc;
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_tree, tree.data(), tree.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
+    if (p->strategy == CVQ_STRATEGY_SWEEP) {
+        // pass 0 covers (lower, sg1] and needs lower <= vmin <= sg0 <= fg <= sg1 <= vmax
+        p->sweep_ok = P.lower <= P.vmin && P.vmin <= P.sg0 && P.sg0 <= P.fg && P.fg <= P.sg1 && P.sg1 <= P.vmax;
+        p->sweep_d0 = std::min(depth, kSweepD0Max);
+        p->sweep_d = std::min(std::max(depth, 1), kSweepDMax);
+        // in-order mids of bracket b's subtree of depth d0 (heap node (l, m) = entry (2m + 1) 2^(d0 - 1 - l) - 1)
+        const int d0 = p->sweep_d0, M0 = (1 << d0) - 1;
+        std::vector<int> l0((size_t)3 * M0 + 3, 0);
+        auto inorder = [&](int b, int o) {
+            for (int k = 0; k < M0; ++k) {
+                int l = d0 - 1, v = k + 1;
+                while (!(v & 1)) { v >>= 1; --l; }
+                const int m = (k + 1) >> (d0 - l);
+                l0[(size_t)o + k] = tree[((size_t)b << depth) + (1 << l) + m];
+            }
+        };
+        l0[0] = p->fixpos[4];                                  // vmin
+        inorder(0, 1);
+        l0[(size_t)M0 + 1] = p->fixpos[1];                     // sg0
+        inorder(1, M0 + 2);
+        l0[(size_t)2 * M0 + 2] = p->fixpos[2];                 // fg
+        inorder(3, 2 * M0 + 3);
+        for (size_t k = 1; k < l0.size() && p->sweep_ok; ++k) p->sweep_ok = l0[k - 1] <= l0[k];
+        if (int rc = dev_alloc(&p->d_sweep0, l0.size())) return rc;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_sweep0, l0.data(), l0.size() * sizeof(int), hipMemcpyHostToDevice,
+                                     p->stream));
+        // node words of [ps, pe) in the sweep's chunk order: (thread t, round r, u) at (r NT + t) 4 + u
+        std::vector<uint32_t> trw0, trw2;
+        auto transpose = [&](int ps, int pe, std::vector<uint32_t>& out) {
+            int a0, L;
+            sweep_chunks(ps, pe, kSortNT, &a0, &L);
+            out.assign((size_t)kSortNT * std::max(L, 4), 0u);
+            for (int t = 0; t < kSortNT; ++t)
+                for (int k = 0; k < L; ++k) {
+                    const size_t pos = (size_t)a0 + (size_t)t * L + k;
+                    out[((size_t)(k / 4) * kSortNT + t) * 4 + k % 4] = pos < p->hidx.size() ? p->hidx[pos] : 0u;
+                }
+        };
+        transpose(p->fixpos[0], p->fixpos[3], trw0);
+        transpose(p->fixpos[3], std::max(p->fixpos[5], p->fixpos[3]), trw2);
+        if (int rc = dev_alloc(&p->d_trw0, trw0.size())) return rc;
+        if (int rc = dev_alloc(&p->d_trw2, trw2.size())) return rc;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_trw0, trw0.data(), trw0.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                     p->stream));
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_trw2, trw2.data(), trw2.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                     p->stream));
+    }
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     p->tree_depth = depth;
     std::memcpy(p->tree_key, key, sizeof key);
@@ -519,9 +572,14 @@ int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G
                    double* snaps, Header* hdr);
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
-                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps);  // cvq_sorted.hip
+                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps,
+                  bool sweep);                                                        // cvq_sorted.hip
 }
 namespace {
+
+bool sorted_family(const cvq_plan* p) {
+    return p->strategy == CVQ_STRATEGY_SORTED || p->strategy == CVQ_STRATEGY_SWEEP;
+}
 
 SortedGeom sorted_geom(const cvq_plan* p) {
     SortedGeom G{};
@@ -531,19 +589,25 @@ SortedGeom sorted_geom(const cvq_plan* p) {
     G.G = (int)p->S.G;
     G.depth = p->tree_depth;
     for (int e = 0; e < 6; ++e) G.fix[e] = p->fixpos[e];
+    G.sweep0 = p->d_sweep0;
+    G.d0 = p->sweep_d0;
+    G.dsweep = p->sweep_d;
+    G.trw0 = p->d_trw0;
+    G.trw2 = p->d_trw2;
     return G;
 }
 
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
-    if (p->strategy == CVQ_STRATEGY_SORTED) {
+    if (sorted_family(p)) {
         int rc = ensure_sorted_tree(p, P);
         if (rc) return rc;
         static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;   // diagnostic phase stamps
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
                              direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
-                             dbg_stamps ? (double*)p->d_stamps : nullptr);
+                             dbg_stamps ? (double*)p->d_stamps : nullptr,
+                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok);
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
@@ -582,10 +646,10 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
 
 int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     TimedScope ts(p, TK_SLAB);
-    if (p->strategy == CVQ_STRATEGY_SORTED) {
+    if (sorted_family(p)) {
         SolveConst P{};
         return launch_sorted(p->S, P, sorted_geom(p), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
-                             direct_fused(p), 1, bounds, out, nullptr, nullptr, nullptr);
+                             direct_fused(p), 1, bounds, out, nullptr, nullptr, nullptr, false);
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {      // COMPACT: slabs of arbitrary bounds run k_direct
         SolveConst P{};
@@ -693,7 +757,7 @@ int ensure_mass(cvq_plan* p, Header* hdr = nullptr) {
 
 // PREFIX and SORTED hold only the nodes with level <= v_cap
 bool materialised(const cvq_plan* p) {
-    return p->strategy == CVQ_STRATEGY_PREFIX || p->strategy == CVQ_STRATEGY_SORTED;
+    return p->strategy == CVQ_STRATEGY_PREFIX || sorted_family(p);
 }
 
 SolveConst solve_const(const cvq_solve_args& a, int K) {
@@ -793,8 +857,10 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
                 CVQ_ERR_INVALID, "NULL static table");
     CVQ_REQUIRE(s->model != CVQ_MSM || s->vol_states != nullptr, CVQ_ERR_INVALID, "MSM needs vol_states");
     CVQ_REQUIRE(s->weights[0] > 0.0, CVQ_ERR_UNSUPPORTED, "weights[0] must be > 0");
-    CVQ_REQUIRE(s->strategy >= CVQ_STRATEGY_PREFIX && s->strategy <= CVQ_STRATEGY_SORTED, CVQ_ERR_INVALID,
+    CVQ_REQUIRE(s->strategy >= CVQ_STRATEGY_PREFIX && s->strategy <= CVQ_STRATEGY_SWEEP, CVQ_ERR_INVALID,
                 "unknown strategy");
+    CVQ_REQUIRE(!(s->strategy == CVQ_STRATEGY_SWEEP && s->dim != 2), CVQ_ERR_UNSUPPORTED,
+                "the SWEEP strategy is built for dim == 2");
     CVQ_REQUIRE(!((s->strategy == CVQ_STRATEGY_DIRECT || s->strategy == CVQ_STRATEGY_COMPACT) && s->dim != 2),
                 CVQ_ERR_UNSUPPORTED, "the DIRECT and COMPACT strategies are built for dim == 2");
     CVQ_REQUIRE(!(s->strategy == CVQ_STRATEGY_SORTED && s->dim == 3 && s->n > 255), CVQ_ERR_UNSUPPORTED,
@@ -927,15 +993,18 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
         S.phi = p->d_phi;
     }
-    if (p->strategy == CVQ_STRATEGY_SORTED) {          // reachable nodes sorted by their exact threshold v*
+    if (sorted_family(p)) {                            // reachable nodes sorted by their exact threshold v*
         std::vector<uint32_t> idx;
         build_sorted_nodes(p->hx, S, kmax, p->hvs, idx);
-        if ((rc = dev_alloc(&p->d_sidx, idx.size())) || (rc = dev_alloc(&p->d_svs, idx.size()))) {
+        const size_t nv = idx.size();
+        p->hidx = idx;
+        idx.resize(((nv + 3) & ~(size_t)3) + 4, 0u);        // SWEEP's 16-B loads read up to 4 words ahead
+        if ((rc = dev_alloc(&p->d_sidx, idx.size())) || (rc = dev_alloc(&p->d_svs, nv))) {
             cvq_plan_destroy(p);
             return rc;
         }
         e = hipMemcpy(p->d_sidx, idx.data(), idx.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(p->d_svs, p->hvs.data(), idx.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_svs, p->hvs.data(), nv * sizeof(double), hipMemcpyHostToDevice);
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT) {         // exact level thresholds + grid lookup buckets
@@ -966,7 +1035,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
                     (void*)p->d_cutfix, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
-                    (void*)p->d_tree})
+                    (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;

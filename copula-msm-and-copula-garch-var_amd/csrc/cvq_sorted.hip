@@ -10,7 +10,6 @@
 namespace cvq {
 namespace {
 
-constexpr int kSortNT = 256;
 
 struct SortedLaunch {
     const StaticDev& S;
@@ -25,10 +24,19 @@ struct SortedLaunch {
     Header* hdr;
     bool fused;
     double* stamps;
+    bool sweep;
 };
 
 template <int COP, bool MSM, int DIM, int PM, bool FUSED, int LAY>
 void launch_l(const SortedLaunch& L) {
+    if constexpr (DIM == 2) {
+        if (L.sweep && L.mode == 0) {                  // SWEEP: one pass per cell (2-D solves)
+            hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY, true>), dim3((unsigned)L.T),
+                               dim3(kSortNT), sorted_lds_bytes(L.S.n, kSortNT, DIM, true), L.stream, L.S, L.P, L.G,
+                               L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY>), dim3((unsigned)L.T), dim3(kSortNT),
                        sorted_lds_bytes(L.S.n, kSortNT, DIM), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode,
                        L.bounds, L.out, L.snaps, L.hdr, L.stamps);
@@ -75,9 +83,9 @@ void launch_c(const SortedLaunch& L) {
 
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
-                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps) {
+                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps, bool sweep) {
     CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
-    const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps};
+    const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
     switch (S.copula) {
         case CVQ_GAUSSIAN: launch_c<CVQ_GAUSSIAN>(L); break;
         case CVQ_STUDENT: launch_c<CVQ_STUDENT>(L); break;

@@ -51,16 +51,43 @@ constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisec
 #endif
 constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
 
+// SWEEP (2-D): boundary list capacity per pass (LDS, double-buffered), the depth of the
+// pass-0 subtrees (3 (2^d0 - 1) + 3 <= cap) and of a later pass's subtree (2^d - 1 <= cap).
+constexpr int kSortNT = 256;                          // threads per k_sorted workgroup
+constexpr int kSweepCap = 256;
+#ifndef CVQ_SWEEP_EDGE
+#define CVQ_SWEEP_EDGE 1
+#endif
+constexpr int kSweepD0Max = 6;
+constexpr int kSweepDMax = 8;
+
 // Date-independent device tables of a SORTED plan.
 struct SortedGeom {
-    const uint32_t* idx;   // [G] packed node indices, sorted by v* (2-D: i0 | j << 16;
-                           //     3-D: a0 | i1 << 9 | j << 17, a0 = i0 + n [i1 == 0], the Q6 plane)
+    const uint32_t* idx;   // [G + pad] packed node indices, sorted by v* (2-D: i0 | j << 16;
+                           //     3-D: a0 | i1 << 9 | j << 17, a0 = i0 + n [i1 == 0], the Q6 plane);
+                           //     padded with zero words to a multiple of 4 (+ 4)
     const double* vs;      // [G] the sorted v*
     const int* tree;       // [4][1 << depth]: ub(mid) of heap node h (1 <= h < 2^depth) of each bracket's tree
     int G;
     int depth;
     int fix[6];            // ub() of lower, sg0, fg, sg1, vmin, vmax
+    // SWEEP: pass 0 covers (lower, sg1]; its sorted boundary list is ub() of vmin, the
+    // in-order mids of bracket 0's tree (depth d0), sg0, bracket 1's mids, fg, bracket 3's mids
+    const int* sweep0;     // [3 (2^d0 - 1) + 3]
+    int d0;                // pass-0 subtree depth
+    int dsweep;            // subtree depth of a later pass
+    // the node words of pass 0's range [fix0, fix3) and of bracket 2's [fix3, fix5) in the
+    // sweep's chunk order, transposed so a wave's round is one coalesced 1-KB load:
+    // word (thread t, round r, u) at [(r NT + t) 4 + u] (sweep_transpose)
+    const uint32_t* trw0;
+    const uint32_t* trw2;
 };
+
+// chunk geometry of a sweep over sorted positions [ps, pe): thread t takes [a0 + t L, a0 + (t + 1) L)
+__host__ __device__ inline void sweep_chunks(int ps, int pe, int nt, int* a0, int* L) {
+    *a0 = ps & ~3;
+    *L = ((pe - *a0 + 4 * nt - 1) / (4 * nt)) * 4;
+}
 
 // exp(x): 2^k e^r, |r| <= ln2 / 2, degree-9 polynomial fitted to exp's relative
 // error on that interval (max 1.4e-14; the solve's decisions are unchanged by 1e-8
@@ -181,9 +208,11 @@ __host__ __device__ inline int sorted_region_doubles(int layout, int n) {
     return layout == kLay2 ? 6 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
 }
 constexpr int kSortScalars = 4;                // flags, arest, last (+ pad), after the reduction slots
-inline size_t sorted_lds_bytes(int n, int nt, int dim) {
+inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false) {
+    // SWEEP: scan slots [NT / 64] + prefix values [2][cap] + boundary positions [2][cap]
+    const size_t sw = sweep ? sizeof(double) * ((size_t)nt / 64 + 2 * kSweepCap) + sizeof(int) * 2 * kSweepCap : 0;
     return sizeof(double) * ((size_t)sorted_region_doubles(sorted_layout(dim, n), n) + 2 * (nt / 64) + kSortScalars) +
-           sizeof(double2) * sorted_tail_cap(dim);
+           sizeof(double2) * sorted_tail_cap(dim) + sw;
 }
 
 // mode 0: calc_var solve (snapshots + header, fused finalize when P.fin_var);
@@ -201,7 +230,14 @@ __host__ __device__ constexpr int sorted_min_waves(int dim) {
     return dim == 2 ? CVQ_SORT_MIN_WAVES2 : CVQ_SORT_MIN_WAVES3;
 }
 
-template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY>
+// SWEEP (2-D): instead of one strided range sum + one workgroup reduction per
+// bisection level, a pass evaluates every node of a cell once -- thread tid sums a contiguous
+// chunk of sorted positions in order -- recording the running sum at each sorted boundary
+// position of the cell's bisection subtree; one scan of the thread totals turns those into
+// prefix sums, and every thread then walks the subtree's levels from LDS (slab = difference of
+// two prefixes) with no further barrier.  Pass 0 covers (lower, sg1], so r0, the second slab
+// and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes one more.
+template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false>
 __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
@@ -232,6 +268,9 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     int& flags = *(int*)(red + 2 * (NT / 64));     // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
     double& s_arest = *(red + 2 * (NT / 64) + 1);  // 3-D: the axis-0 weight off the plane i1 == 0
     int& last = *(int*)(red + 2 * (NT / 64) + 2);  // fused finalize: this workgroup is the last
+    double* sred = red + 2 * (NT / 64) + kSortScalars;   // SWEEP: [NT / 64] scan slots
+    double* Pvs = sred + NT / 64;                  // SWEEP: [2][kSweepCap] prefix values
+    int* Bls = (int*)(Pvs + 2 * kSweepCap);        // SWEEP: [2][kSweepCap] boundary positions
 
     // diagnostic phase stamps (CVQ_STAMPS=1, never in a timed run): COMPACT's slots --
     // 0 start, 1 tables, 2 first slab, 3 second slab, 4 bracket, 5 + level, 29 tail
@@ -300,6 +339,9 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         s_arest = s0;
     }
     if (tid == 0 && lds_base(lds) != 0) bad |= 4;          // packed offsets need the region at LDS 0
+    if constexpr (SWEEP) {                                 // pass 0's boundary list -> buffer 0
+        for (int k = tid; k < 3 * ((1 << G.d0) - 1) + 3; k += NT) Bls[k] = G.sweep0[k];
+    }
     if (bad) atomicOr(&flags, bad);
     __syncthreads();
     const int fl = flags;
@@ -511,16 +553,123 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         return v == P.lower ? G.fix[0] : v == P.sg0 ? G.fix[1] : v == P.fg ? G.fix[2]
              : v == P.sg1 ? G.fix[3] : v == P.vmin ? G.fix[4] : G.fix[5];
     };
+    // SWEEP pass: the nodes at sorted positions [ps, pe) summed once, thread tid taking the
+    // contiguous chunk [s, s + L) (L a multiple of 4, chunks aligned to 4 positions: one
+    // 16-B index load per 4 nodes) in position order; Pv[i] = sum of the nodes before sorted
+    // position Bl[i] (Bl sorted, ps <= Bl[i] <= pe).  Returns the cell total; ends with a barrier.
+    auto sweep = [&](int ps, int pe, const int* Bl, double* Pv, int M, const uint32_t* trw) -> double {
+        int a0, L;
+        sweep_chunks(ps, pe, NT, &a0, &L);
+        const int s = a0 + tid * L, e = min(s + L, pe);
+        const int eown = tid == NT - 1 ? 0x7FFFFFFF : s + L;   // boundaries in [s, eown) are mine
+        int i = 0;
+        for (int hiI = M; i < hiI;) {                      // first boundary >= s
+            const int md = (i + hiI) >> 1;
+            if (Bl[md] < s) i = md + 1; else hiI = md;
+        }
+        const int i0 = i;
+        int nb = i < M ? Bl[i] : 0x7FFFFFFF;
+        double acc = 0.0;
+        if (fast) {
+            // the next round's 4 node words are loaded while this round computes (a lane's
+            // chunk is its own cache lines: the loads do not coalesce across the wave)
+            // (natural order) or one coalesced load per wave (transposed copy)
+            const uint4* wp = trw ? (const uint4*)trw + tid : (const uint4*)(G.idx + s);
+            const int wst = trw ? NT : 1;                  // uint4 stride between rounds
+            uint4 wn = s < e ? wp[0] : make_uint4(0u, 0u, 0u, 0u);
+            for (int p = s; p < e; p += 4) {
+                const uint4 w = wn;
+                wp += wst;
+                if (p + 4 < e) wn = *wp;
+                const uint32_t c[4] = {w.x, w.y, w.z, w.w};
+                double v[4];
+                if (CVQ_SWEEP_EDGE == 0 || (p >= ps && p + 4 <= pe)) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = node_fast(c[u]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = (p + u >= ps && p + u < pe) ? node_fast(c[u]) : 0.0;
+                }
+                if (nb < p + 4) {                          // a boundary inside this round
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        while (nb == p + u) {
+                            Pv[i] = acc;
+                            ++i;
+                            nb = i < M ? Bl[i] : 0x7FFFFFFF;
+                        }
+                        acc += v[u];
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc += v[u];
+                }
+            }
+        } else {                                           // reference-semantics nodes, one at a time
+            for (int p = max(s, ps); p < e; ++p) {
+                while (nb == p) {
+                    Pv[i] = acc;
+                    ++i;
+                    nb = i < M ? Bl[i] : 0x7FFFFFFF;
+                }
+                acc += node_generic(G.idx[p]);
+            }
+        }
+        while (nb < eown) {                                // boundaries past my last node
+            Pv[i] = acc;
+            ++i;
+            nb = i < M ? Bl[i] : 0x7FFFFFFF;
+        }
+        // exclusive scan of the thread totals (fixed order: identical in every thread)
+        double x = acc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        const double xe = __shfl_up(x, 1, 64);
+        if (lane == 63) sred[tid >> 6] = x;
+        __syncthreads();
+        double base = lane == 0 ? 0.0 : xe, total = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) {
+            const double sw = sred[w];
+            if (w < (tid >> 6)) base += sw;
+            total += sw;
+        }
+        for (int k = i0; k < i; ++k) Pv[k] += base;
+        __syncthreads();
+        return total;
+    };
+
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));                 // (lower, fg]
-    stamp(2);
-    nodes += max(G.fix[2] - G.fix[0], 0);
-    const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-    const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+    double r0, nr;
+    double tot0 = 0.0, Pvmin = 0.0, Psg0 = 0.0, Pfg = 0.0;   // SWEEP pass-0 prefixes
+    const int M0 = (1 << G.d0) - 1;
+    double nl, nu;
+    if constexpr (SWEEP) {
+        tot0 = sweep(G.fix[0], G.fix[3], Bls, Pvs, 3 * M0 + 3, G.trw0);
+        Pvmin = Pvs[0];
+        Psg0 = Pvs[M0 + 1];
+        Pfg = Pvs[2 * M0 + 2];
+        r0 = Pfg;                                          // (lower, fg]
+        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        nr = (nl == P.fg) ? tot0 - Pfg : Pfg - Psg0;        // (fg, sg1] or (sg0, fg]
+        stamp(2);
+        stamp(3);
+        nodes += G.fix[3] - G.fix[0];
+    } else {
+        r0 = team_sum(range_sum(G.fix[0], G.fix[2]));                 // (lower, fg]
+        stamp(2);
+        nodes += max(G.fix[2] - G.fix[0], 0);
+        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+        stamp(3);
+        nodes += max(fixpos(nu) - fixpos(nl), 0);
+    }
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
-    stamp(3);
-    nodes += max(fixpos(nu) - fixpos(nl), 0);
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     double lo = __builtin_nan(""), hi = __builtin_nan("");
     int br = -1;                                           // bracket (tree) index; -1: NaN bracket (Q3)
@@ -541,6 +690,69 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     int nt = -1, it = 0;
     uint64_t mask = 0;
     double* sn = snaps + t * P.stride;
+    if constexpr (SWEEP) {
+        // levels of the subtree (depth Ds) whose in-order boundary list starts at Bl + o:
+        // heap node (level l, path m) is entry (2m + 1) 2^(Ds - 1 - l) - 1
+        auto descend = [&](const int* Bl, const double* Pv, int o, int Ds, double Plo, double Phi) {
+            int m = 0;
+            for (int l = 0; l < Ds && it < P.K && phi - plo > TCAP; ++l, ++it) {
+                const double mid = (lo + hi) / 2;
+                if (tid == 0) sn[it] = mid;
+                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+                const int ii = o + ((2 * m + 1) << (Ds - 1 - l)) - 1;
+                const int pm = Bl[ii];
+                const double Pm = Pv[ii];
+                const double val = ustack ? Pm - Plo : Phi - Pm;
+                const double slab_lower = ustack ? lo : mid;
+                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
+                if (Fn != 0.0) mask |= (1ull << it);
+                ustack = Fn < P.obj;
+                if (ustack) { lo = mid; plo = pm; Plo = Pm; m = 2 * m + 1; }
+                else        { hi = mid; phi = pm; Phi = Pm; m = 2 * m; }
+                h = 2 * h + (ustack ? 1 : 0);
+                prev = Fn;
+                prevU = mid;
+            }
+        };
+        if (br == 0) descend(Bls, Pvs, 1, G.d0, Pvmin, Psg0);
+        else if (br == 1) descend(Bls, Pvs, M0 + 2, G.d0, Psg0, Pfg);
+        else if (br == 3) descend(Bls, Pvs, 2 * M0 + 3, G.d0, Pfg, tot0);
+        int buf = 0;
+        while (it < P.K && phi - plo > TCAP) {
+            const int lvl = 31 - __builtin_clz(h);
+            if (h < tsz) {                                 // one pass over the cell (lo, hi]
+                const int Ds = min(G.dsweep, G.depth - lvl);
+                const int M = (1 << Ds) - 1;
+                buf ^= 1;
+                int* Bl = Bls + buf * kSweepCap;
+                double* Pv = Pvs + buf * kSweepCap;
+                for (int k = tid; k < M; k += NT) {         // in-order entry k -> heap node
+                    const int l = Ds - 1 - __builtin_ctz(k + 1), m = (k + 1) >> (Ds - l);
+                    Bl[k] = tr[(h << l) + m];
+                }
+                __syncthreads();
+                const double tot = sweep(plo, phi, Bl, Pv, M, (h == 1 && br == 2) ? G.trw2 : nullptr);
+                nodes += phi - plo;
+                descend(Bl, Pv, 0, Ds, 0.0, tot);
+            } else {                                       // beyond the tabulated tree: one level
+                const double mid = (lo + hi) / 2;
+                if (tid == 0) sn[it] = mid;
+                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+                const int pm = sorted_ub(G.vs, plo, phi, mid);
+                const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
+                nodes += ustack ? pm - plo : phi - pm;
+                const double slab_lower = ustack ? lo : mid;
+                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
+                if (Fn != 0.0) mask |= (1ull << it);
+                ustack = Fn < P.obj;
+                if (ustack) { lo = mid; plo = pm; }
+                else        { hi = mid; phi = pm; }
+                prev = Fn;
+                prevU = mid;
+                ++it;
+            }
+        }
+    } else {
     for (; it < P.K && phi - plo > TCAP; ++it) {
         const double mid = (lo + hi) / 2;
         if (tid == 0) sn[it] = mid;
@@ -563,6 +775,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         if (it < 15) stamp(5 + it);
         prev = Fn;
         prevU = mid;
+    }
     }
 
     // ---- tail: the bracket's <= TCAP nodes -> LDS, wave 0 finishes the levels

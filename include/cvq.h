@@ -50,6 +50,8 @@ extern "C" {
 #define CVQ_STRATEGY_COMPACT 2   /* DIRECT control flow, one barrier per level, one-wave tail */
 #define CVQ_STRATEGY_SORTED 3    /* reachable nodes sorted by membership threshold: a slab is
                                     one contiguous range (2-D, and 3-D with n <= 255)       */
+#define CVQ_STRATEGY_SWEEP 4     /* SORTED's node order, each bisection cell summed in one pass
+                                    with prefix sums at its subtree's mids (2-D)            */
 
 typedef struct cvq_plan cvq_plan;
 

@@ -70,12 +70,12 @@ def test_special_functions_vs_scipy_and_mpmath():
     assert np.max(np.abs(got - k["erf"])) <= 2.3e-16
 
 
-STRATEGIES = ["prefix", "direct", "compact", "sorted"]
+STRATEGIES = ["prefix", "direct", "compact", "sorted", "sweep"]
 
 
 def _skip_unsupported(z, strategy):
-    if strategy in ("direct", "compact") and int(z["dim"]) != 2:
-        pytest.skip("DIRECT and COMPACT strategies are built for dim == 2")
+    if strategy in ("direct", "compact", "sweep") and int(z["dim"]) != 2:
+        pytest.skip("DIRECT, COMPACT and SWEEP strategies are built for dim == 2")
 
 
 @pytest.mark.parametrize("strategy", STRATEGIES)

@@ -96,18 +96,35 @@ def test_3d_sorted_matches_prefix_many_dates():
 def test_cfg2_full_size_sorted_matches_compact():
     c, ipt, uvs, ggp, ptf = _workload(2, 1000)
     out = {}
-    for strategy in ("compact", "sorted"):
+    for strategy in ("compact", "sorted", "sweep"):
         p = _plan(c, ipt, uvs, ggp, strategy)
         try:
             out[strategy] = p.calc_var(ptf)
         finally:
             p.close()
-    assert out["compact"][1] == out["sorted"][1]
-    assert np.array_equal(out["compact"][0], out["sorted"][0])
+    for strategy in ("sorted", "sweep"):
+        assert out["compact"][1] == out[strategy][1]
+        assert np.array_equal(out["compact"][0], out[strategy][0]), strategy
 
 
-@pytest.mark.parametrize("case", ["cfg4_k4_n16", "cfg2_n64"])
-def test_generic_path_non_rank1_pi(case):
+@pytest.mark.parametrize("cfg,T", [(1, 50), (3, 1000), (5, 1000)])
+def test_full_size_sweep_matches_sorted(cfg, T):
+    """SWEEP (one pass per bisection cell, slabs as prefix differences) against SORTED
+    (one strided range sum per level) at the BASELINE geometries: bit-identical VaR."""
+    c, ipt, uvs, ggp, ptf = _workload(cfg, T)
+    out = {}
+    for strategy in ("sorted", "sweep"):
+        p = _plan(c, ipt, uvs, ggp, strategy)
+        try:
+            out[strategy] = p.calc_var(ptf)
+        finally:
+            p.close()
+    assert out["sorted"][1] == out["sweep"][1]
+    assert np.array_equal(out["sorted"][0], out["sweep"][0])
+
+
+@pytest.mark.parametrize("case,strategy", [("cfg4_k4_n16", "sorted"), ("cfg2_n64", "sorted"), ("cfg2_n64", "sweep")])
+def test_generic_path_non_rank1_pi(case, strategy):
     """A pi that is not the product of per-asset forecasts forces the generic node
     path (full W contraction, create_grids.py:121-171); VaR must follow the oracle."""
     from copula_var.engine import QuadraturePlan
@@ -121,7 +138,7 @@ def test_generic_path_non_rank1_pi(case):
             z["combos"], z["weights"], z["copula_params"])
     P = Problem(*args, (fbs, pi), z["unique_vol_states"])
     ref, ref_it, _ = calc_var(P.compute_integral, P.T, float(z["ptf_mean"]))
-    p = QuadraturePlan(*args, vol_states=z["unique_vol_states"], strategy="sorted")
+    p = QuadraturePlan(*args, vol_states=z["unique_vol_states"], strategy=strategy)
     try:
         p.set_dates((fbs, pi))
         var, it = p.calc_var(float(z["ptf_mean"]))
@@ -133,8 +150,10 @@ def test_generic_path_non_rank1_pi(case):
     assert np.array_equal(var, ref)
 
 
-@pytest.mark.parametrize("case,ranks", [("cfg4_k6_n16", 2), ("cfg2_n64", 3), ("cfg1", 2)])
-def test_sharded_sorted(case, ranks):
+@pytest.mark.parametrize("case,ranks,strategy", [("cfg4_k6_n16", 2, "sorted"), ("cfg2_n64", 3, "sorted"),
+                                                 ("cfg1", 2, "sorted"), ("cfg2_n64", 3, "sweep"),
+                                                 ("cfg1", 2, "sweep")])
+def test_sharded_sorted(case, ranks, strategy):
     from copula_var import engine
     from copula_var.distributed import shard
     from copula_var.engine import QuadraturePlan
@@ -154,7 +173,7 @@ def test_sharded_sorted(case, ranks):
                 continue
             p = QuadraturePlan(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"],
                                z["densities"], z["combos"], z["weights"], z["copula_params"],
-                               vol_states=z.get("unique_vol_states"), strategy="sorted")
+                               vol_states=z.get("unique_vol_states"), strategy=strategy)
             p.set_stream(torch.cuda.current_stream().cuda_stream)
             if str(z["model"]) == "msm":
                 p.set_dates((z["forecasts_by_states"][lo:hi], z["forecasts"][lo:hi]))
@@ -169,6 +188,26 @@ def test_sharded_sorted(case, ranks):
     finally:
         for p in plans:
             p.close()
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(first_guess=-2.5, second_guess=(-4.0, -1.5)),
+                                dict(first_guess=-1.0, second_guess=(-2.0, -0.5), min_var=-5.0),
+                                dict(first_guess=-3.0, second_guess=(-2.0, -3.5)),      # unordered: SORTED path
+                                dict(obj_var=0.01), dict(obj_var=0.2)])
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_sweep_matches_sorted_solve_arguments(cfg, kw):
+    """SWEEP against SORTED for non-default calc_var arguments (other brackets, other
+    objectives; unordered guesses fall back to the per-level loop): bit-identical."""
+    c, ipt, uvs, ggp, ptf = _workload(cfg, 300, n=96)
+    out = {}
+    for strategy in ("sorted", "sweep"):
+        p = _plan(c, ipt, uvs, ggp, strategy)
+        try:
+            out[strategy] = p.calc_var(ptf, **kw)
+        finally:
+            p.close()
+    assert out["sorted"][1] == out["sweep"][1]
+    np.testing.assert_array_equal(out["sorted"][0], out["sweep"][0])
 
 
 def test_sorted_rejects_levels_above_v_cap():
