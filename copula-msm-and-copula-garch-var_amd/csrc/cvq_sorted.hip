@@ -32,19 +32,22 @@ void launch_l(const SortedLaunch& L) {
     if constexpr (DIM == 2) {
         if (L.sweep && L.mode == 0) {                  // SWEEP: one pass per cell (2-D solves)
             hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY, true>), dim3((unsigned)L.T),
-                               dim3(kSortNT), sorted_lds_bytes(L.S.n, kSortNT, DIM, true), L.stream, L.S, L.P, L.G,
-                               L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
+                               dim3(kSortNT), sorted_lds_bytes(L.S.n, kSortNT, DIM, true, LAY), L.stream, L.S, L.P,
+                               L.G, L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
             return;
         }
     }
     hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY>), dim3((unsigned)L.T), dim3(kSortNT),
-                       sorted_lds_bytes(L.S.n, kSortNT, DIM), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode,
-                       L.bounds, L.out, L.snaps, L.hdr, L.stamps);
+                       sorted_lds_bytes(L.S.n, kSortNT, DIM, false, LAY), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB,
+                       L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
 }
 
 template <int COP, bool MSM, int DIM, int PM, bool FUSED>
 void launch_f(const SortedLaunch& L) {
     if constexpr (DIM == 2) {
+        if constexpr (COP == CVQ_STUDENT && PM > 0) {
+            if (L.G.layout == kLay2W) { launch_l<COP, MSM, DIM, PM, FUSED, kLay2W>(L); return; }
+        }
         launch_l<COP, MSM, DIM, PM, FUSED, kLay2>(L);
     } else {
         if (sorted_layout(DIM, L.S.n) == kLay3F) launch_l<COP, MSM, DIM, PM, FUSED, kLay3F>(L);

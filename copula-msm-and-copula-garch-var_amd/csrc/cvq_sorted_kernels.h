@@ -54,6 +54,9 @@ constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thr
 // SWEEP (2-D): boundary list capacity per pass (LDS, double-buffered), the depth of the
 // pass-0 subtrees (3 (2^d0 - 1) + 3 <= cap) and of a later pass's subtree (2^d - 1 <= cap).
 constexpr int kSortNT = 256;                          // threads per k_sorted workgroup
+#ifndef CVQ_SWEEP_MIN_WAVES
+#define CVQ_SWEEP_MIN_WAVES 4                         // SWEEP: <= 128 VGPRs (the pass loop holds the solve state)
+#endif
 constexpr int kSweepCap = 256;
 #ifndef CVQ_SWEEP_EDGE
 #define CVQ_SWEEP_EDGE 1
@@ -81,6 +84,7 @@ struct SortedGeom {
     // word (thread t, round r, u) at [(r NT + t) 4 + u] (sweep_transpose)
     const uint32_t* trw0;
     const uint32_t* trw2;
+    int layout;            // node-word layout (sorted_pack): kLay2W for folded Student records
 };
 
 // chunk geometry of a sweep over sorted positions [ps, pe): thread t takes [a0 + t L, a0 + (t + 1) L)
@@ -151,7 +155,18 @@ __device__ __forceinline__ int sorted_ub(const double* __restrict__ vs, int lo, 
 //           i1 in bits 12-18 (32-B axis-1 records), j in bits 25-31 (j * 16)
 //   kLay3G  (3-D, n <= 255): a0 | i1 << 9 | j << 17, record indices
 // with a0 = i0 + n on the plane i1 == 0 (Q6), whose axis-0 records are separate.
-enum { kLay2 = 0, kLay3F = 1, kLay3G = 2 };
+//   kLay2W  (2-D, SWEEP Student with an integer power): as kLay2 with 32-B records holding the
+//           folded scale, off0 = 32 i0, off2 = 32 (ns + j) (see node_fast)
+enum { kLay2 = 0, kLay3F = 1, kLay3G = 2, kLay2W = 3 };
+// the plans whose SWEEP solve uses kLay2W: 2-D Student with nu = 6 (b^-4, the launcher's PM = 8)
+__host__ __device__ constexpr bool sorted_fold(int copula, int dim, int node_m) {
+    return copula == CVQ_STUDENT && dim == 2 && node_m == dim + 6;
+}
+__host__ __device__ constexpr double pow2_constexpr(int e) {
+    double r = 1.0;
+    for (int k = 0; k < e; ++k) r *= 2.0;
+    return r;
+}
 constexpr int kLay3FMaxN = 128;
 constexpr int kLay3FAx1 = 4096, kLay3FAx2 = 8192, kLay3FBytes = 10240;   // byte offsets / size of its region
 __host__ __device__ constexpr int sorted_layout(int dim, int n) {
@@ -159,8 +174,9 @@ __host__ __device__ constexpr int sorted_layout(int dim, int n) {
 }
 inline uint32_t sorted_pack(int layout, int n, int i0, int i1, int j) {
     const int ns = (n + 1) & ~1;
-    const int a0 = i0 + (layout != kLay2 && i1 == 0 ? n : 0);
+    const int a0 = i0 + (layout != kLay2 && layout != kLay2W && i1 == 0 ? n : 0);
     if (layout == kLay2) return (uint32_t)(16 * i0) | ((uint32_t)(16 * (ns + j)) << 16);
+    if (layout == kLay2W) return (uint32_t)(32 * i0) | ((uint32_t)(32 * (ns + j)) << 16);
     if (layout == kLay3F) return ((uint32_t)a0 << 4) | ((uint32_t)i1 << 12) | ((uint32_t)j << 25);
     return (uint32_t)a0 | ((uint32_t)i1 << 9) | ((uint32_t)j << 17);
 }
@@ -182,6 +198,10 @@ __device__ __forceinline__ void unpack_node(uint32_t c, int ns, int* a0, int* i1
         *a0 = (int)(c & 0xFFFFu) >> 4;
         *i1 = 0;
         *j = ((int)(c >> 16) >> 4) - ns;
+    } else if constexpr (LAY == kLay2W) {
+        *a0 = (int)(c & 0xFFFFu) >> 5;
+        *i1 = 0;
+        *j = ((int)(c >> 16) >> 5) - ns;
     } else if constexpr (LAY == kLay3F) {
         *a0 = (int)__builtin_amdgcn_ubfe(c, 4, 8);
         *i1 = (int)__builtin_amdgcn_ubfe(c, 12, 7);
@@ -205,13 +225,14 @@ inline int sorted_stride(int n) { return (n + 1) & ~1; }
 // doubles of the table region
 __host__ __device__ inline int sorted_region_doubles(int layout, int n) {
     const int ns = (n + 1) & ~1;
-    return layout == kLay2 ? 6 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
+    return layout == kLay2 ? 6 * ns : layout == kLay2W ? 8 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
 }
 constexpr int kSortScalars = 4;                // flags, arest, last (+ pad), after the reduction slots
-inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false) {
+inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false, int layout = -1) {
+    if (layout < 0) layout = sorted_layout(dim, n);
     // SWEEP: scan slots [NT / 64] + prefix values [2][cap] + boundary positions [2][cap]
     const size_t sw = sweep ? sizeof(double) * ((size_t)nt / 64 + 2 * kSweepCap) + sizeof(int) * 2 * kSweepCap : 0;
-    return sizeof(double) * ((size_t)sorted_region_doubles(sorted_layout(dim, n), n) + 2 * (nt / 64) + kSortScalars) +
+    return sizeof(double) * ((size_t)sorted_region_doubles(layout, n) + 2 * (nt / 64) + kSortScalars) +
            sizeof(double2) * sorted_tail_cap(dim) + sw;
 }
 
@@ -238,7 +259,7 @@ __host__ __device__ constexpr int sorted_min_waves(int dim) {
 // two prefixes) with no further barrier.  Pass 0 covers (lower, sg1], so r0, the second slab
 // and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes one more.
 template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false>
-__global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
+__global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
                                                const double* __restrict__ bounds, double* __restrict__ out,
@@ -258,7 +279,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
     double* wg = Bg + DIM * ns;                    // generic [DIM][n]
     double* fr0 = lds;                             // fast [ns (3-D: 2 ns)][2] axis 0
     // axis 1 (3-D): kLay3F 32-B records (c01 z1, c12 z1, g1 | z1, B'1); kLay3G [ns][2] + fg1 [ns]
-    double* fr1 = LAY == kLay3F ? lds + kLay3FAx1 / 8 : fr0 + (DIM == 3 ? 4 : 2) * ns;
+    double* fr1 = LAY == kLay3F ? lds + kLay3FAx1 / 8 : fr0 + (DIM == 3 || LAY == kLay2W ? 4 : 2) * ns;
     double* fg1 = LAY == kLay3F ? fr1 + 2 : fr1 + (DIM == 3 ? 2 : 0) * ns;
     constexpr int R1 = LAY == kLay3F ? 4 : 2;      // doubles per axis-1 record
     constexpr int FG = LAY == kLay3F ? 4 : 1;      // fg1 stride
@@ -386,6 +407,20 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
                 fr1[R1 * i + 1] = k12 * z;
                 fg1[FG * i] = lg(B * w) + kcc;
             }
+        } else if (LAY == kLay2W) {                        // Student, folded scale s = sc^(-2/m)
+            const double sc = (ax == 0 ? S.term1 : 1.0) * B * w;
+            const double sf = PM == 8 ? 1.0 / sqrt(sqrt(sc)) : pow(sc, -2.0 / (PM > 0 ? PM : 1));
+            double* r = ax == 0 ? fr0 + 4 * i : fr2 + 4 * i;
+            if (ax == 0) {                                 // b' = X . Y = s0 s2 (1 + z^T R^-1 z / nu)
+                r[0] = sf * fma(kq * S.Ri[0], z * z, 1.0);
+                r[1] = sf * (k02 * z);
+                r[2] = sf;
+            } else {
+                r[0] = sf;
+                r[1] = sf * z;
+                r[2] = sf * (kq * S.Ri[3] * (z * z));
+            }
+            r[3] = 0.0;
         } else {                                           // Student: z and scale; Plackett: u and scale
             const double sc = (ax == 0 && COP == CVQ_STUDENT ? S.term1 : 1.0) * B *
                               (ax == 0 && DIM == 3 ? arest : w);
@@ -410,7 +445,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         return make_double2(v.x, v.y);
     };
     auto rec0 = [&](uint32_t c) -> const lds_f64* {
-        if constexpr (LAY == kLay2) return lds_at(c & 0xFFFFu);
+        if constexpr (LAY == kLay2 || LAY == kLay2W) return lds_at(c & 0xFFFFu);
         else if constexpr (LAY == kLay3F) return lds_at(c & 0xFF0u);
         else return lds_at(lds_base(fr0) + 16 * __builtin_amdgcn_ubfe(c, 0, 9));
     };
@@ -419,9 +454,30 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         else return lds_at(lds_base(fr1) + 16 * __builtin_amdgcn_ubfe(c, 9, 8));
     };
     auto rec2 = [&](uint32_t c) -> const lds_f64* {
-        if constexpr (LAY == kLay2) return lds_at(c >> 16);
+        if constexpr (LAY == kLay2 || LAY == kLay2W) return lds_at(c >> 16);
         else if constexpr (LAY == kLay3F) return lds_at(kLay3FAx2 + (c >> 21));
         else return lds_at(lds_base(fr2) + 16 * (c >> 17));
+    };
+    constexpr double kFoldClamp = pow2_constexpr(2000 / (PM > 0 ? PM : 2000));
+    // 2-D node from its two 16-B records (kLay2): the sweep issues a round's LDS reads first
+    auto node2 = [&](const double2 A, const double2 C) -> double {
+        if constexpr (COP == CVQ_GAUSSIAN) {
+            return exp_node(fma(A.x, C.x, A.y + C.y));
+        } else if constexpr (COP == CVQ_STUDENT) {
+            const double b = fma(A.x, fma(a00, A.x, k02 * C.x), fma(a22 * C.x, C.x, 1.0));
+            return (A.y * C.y) * pow_fast<PM>(b, S.node_m, S.node_ex);
+        } else {
+            const double th = S.theta, a1 = th - 1.0, u = A.x, v = C.x, s2 = u + v;
+            const double num = th * fma(a1, fma(-2.0 * u, v, s2), 1.0);
+            const double d = fma(a1, s2, 1.0) * fma(-a1, s2, 1.0 + a1);
+            const double den = d * d;
+            double y = __builtin_amdgcn_rcp(den);
+            y = fma(y, fma(-den, y, 1.0), y);
+            y = fma(y, fma(-den, y, 1.0), y);
+            const double c0 = den == 0.0 ? (num == 0.0 ? __builtin_nan("") : __builtin_copysign(__builtin_inf(), num))
+                                         : num * y;
+            return c0 * (A.y * C.y);
+        }
     };
     auto node_fast = [&](uint32_t c) -> double {
         const double2 A = rd2(rec0(c));
@@ -435,6 +491,15 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
                 const double g1 = LAY == kLay3F ? r1[2] : fg1[__builtin_amdgcn_ubfe(c, 9, 8)];
                 return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
             }
+        } else if constexpr (COP == CVQ_STUDENT && LAY == kLay2W) {
+            // node = sc0 sc2 b^(-m/2) = b'^(-m/2), b' = s0 s2 b = X0 Y0 + X1 Y1 + X2 Y2 (records
+            // hold s = sc^(-2/m)); b' is clamped below 2^(2000/m) so b'^(m/2) stays finite
+            // (the node is then < 2^-1000 instead of its denormal / zero value)
+            const lds_f64* ra = rec0(c);
+            const lds_f64* rc = rec2(c);
+            const double2 X = rd2(ra), Y = rd2(rc);
+            const double b = fmin(fma(X.x, Y.x, fma(X.y, Y.y, ra[2] * rc[2])), kFoldClamp);
+            return pow_fast<PM>(b, S.node_m, S.node_ex);
         } else if constexpr (COP == CVQ_STUDENT) {
             double b, sc;
             if constexpr (DIM == 2) {
@@ -568,49 +633,73 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
             if (Bl[md] < s) i = md + 1; else hiI = md;
         }
         const int i0 = i;
-        int nb = i < M ? Bl[i] : 0x7FFFFFFF;
+        int nb = i < M ? Bl[i] : 0x7FFFFFFF;             // my next boundary, and the one after it
+        int nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;     // (loaded a boundary ahead: no LDS wait in the loop)
         double acc = 0.0;
         if (fast) {
-            // the next round's 4 node words are loaded while this round computes (a lane's
-            // chunk is its own cache lines: the loads do not coalesce across the wave)
-            // (natural order) or one coalesced load per wave (transposed copy)
-            const uint4* wp = trw ? (const uint4*)trw + tid : (const uint4*)(G.idx + s);
-            const int wst = trw ? NT : 1;                  // uint4 stride between rounds
-            uint4 wn = s < e ? wp[0] : make_uint4(0u, 0u, 0u, 0u);
-            for (int p = s; p < e; p += 4) {
-                const uint4 w = wn;
-                wp += wst;
-                if (p + 4 < e) wn = *wp;
+            // node words: the root passes read a transposed copy (one coalesced 1-KB load per
+            // wave and round); deeper passes the solve order (a lane's chunk is its own lines)
+            auto word4 = [&](int p) {                      // the 4 node words of the round at position p
+                return trw ? ((const uint4*)trw)[tid + (size_t)((p - s) >> 2) * NT] : *(const uint4*)(G.idx + p);
+            };
+            // a round's 4 node values: every LDS read issued before the arithmetic
+            auto vals = [&](const uint4 w, double (&v)[4]) {
                 const uint32_t c[4] = {w.x, w.y, w.z, w.w};
-                double v[4];
-                if (CVQ_SWEEP_EDGE == 0 || (p >= ps && p + 4 <= pe)) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = node_fast(c[u]);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = (p + u >= ps && p + u < pe) ? node_fast(c[u]) : 0.0;
-                }
-                if (nb < p + 4) {                          // a boundary inside this round
+                if constexpr (LAY == kLay2) {
+                    double2 A[4], C[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        while (nb == p + u) {
-                            Pv[i] = acc;
-                            ++i;
-                            nb = i < M ? Bl[i] : 0x7FFFFFFF;
-                        }
-                        acc += v[u];
+                        A[u] = rd2(rec0(c[u]));
+                        C[u] = rd2(rec2(c[u]));
                     }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = node2(A[u], C[u]);
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) acc += v[u];
+                    for (int u = 0; u < 4; ++u) v[u] = node_fast(c[u]);
                 }
+            };
+            // add a round's values in position order, recording the running sum at my boundaries
+            // in it (a boundary's prefix is exactly the running sum the later rounds continue)
+            auto round_add = [&](int p, const double (&v)[4]) {
+                const double s1 = acc + v[0], s2 = s1 + v[1], s3 = s2 + v[2];
+                while (nb < p + 4) {                       // divergent but short: no loads waited on
+                    const int off = nb - p;
+                    Pv[i] = off == 0 ? acc : off == 1 ? s1 : off == 2 ? s2 : s3;
+                    ++i;
+                    nb = nb2;
+                    nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
+                }
+                acc = s3 + v[3];
+            };
+            auto partial = [&](int p) {                    // a round with positions outside [ps, pe)
+                double v[4];
+                vals(word4(p), v);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = (p + u >= ps && p + u < pe) ? v[u] : 0.0;
+                round_add(p, v);
+            };
+            int p = s;
+            if (p < e && p < ps) {                         // thread 0's first round (ps not 4-aligned)
+                partial(p);
+                p += 4;
             }
+            uint4 wn = p + 4 <= e ? word4(p) : make_uint4(0u, 0u, 0u, 0u);
+            for (; p + 4 <= e; p += 4) {                   // full rounds; the next round's words in flight
+                const uint4 w = wn;
+                if (p + 8 <= e) wn = word4(p + 4);
+                double v[4];
+                vals(w, v);
+                round_add(p, v);
+            }
+            if (p < e) partial(p);                         // the last active thread's last round
         } else {                                           // reference-semantics nodes, one at a time
             for (int p = max(s, ps); p < e; ++p) {
                 while (nb == p) {
                     Pv[i] = acc;
                     ++i;
-                    nb = i < M ? Bl[i] : 0x7FFFFFFF;
+                    nb = nb2;
+                    nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
                 }
                 acc += node_generic(G.idx[p]);
             }
@@ -618,7 +707,8 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         while (nb < eown) {                                // boundaries past my last node
             Pv[i] = acc;
             ++i;
-            nb = i < M ? Bl[i] : 0x7FFFFFFF;
+            nb = nb2;
+            nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
         }
         // exclusive scan of the thread totals (fixed order: identical in every thread)
         double x = acc;
@@ -642,140 +732,140 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM)) void k_sorted(StaticDev 
         return total;
     };
 
-    // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    double r0, nr;
-    double tot0 = 0.0, Pvmin = 0.0, Psg0 = 0.0, Pfg = 0.0;   // SWEEP pass-0 prefixes
-    const int M0 = (1 << G.d0) - 1;
-    double nl, nu;
-    if constexpr (SWEEP) {
-        tot0 = sweep(G.fix[0], G.fix[3], Bls, Pvs, 3 * M0 + 3, G.trw0);
-        Pvmin = Pvs[0];
-        Psg0 = Pvs[M0 + 1];
-        Pfg = Pvs[2 * M0 + 2];
-        r0 = Pfg;                                          // (lower, fg]
-        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-        nu = (r0 < P.obj) ? P.sg1 : P.fg;
-        nr = (nl == P.fg) ? tot0 - Pfg : Pfg - Psg0;        // (fg, sg1] or (sg0, fg]
-        stamp(2);
-        stamp(3);
-        nodes += G.fix[3] - G.fix[0];
-    } else {
-        r0 = team_sum(range_sum(G.fix[0], G.fix[2]));                 // (lower, fg]
-        stamp(2);
-        nodes += max(G.fix[2] - G.fix[0], 0);
-        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-        nu = (r0 < P.obj) ? P.sg1 : P.fg;
-        nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
-        stamp(3);
-        nodes += max(fixpos(nu) - fixpos(nl), 0);
-    }
-    const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
+    // solve state (calc_var_class.py:114-160 and the bisection's :250-309)
     double lo = __builtin_nan(""), hi = __builtin_nan("");
     int br = -1;                                           // bracket (tree) index; -1: NaN bracket (Q3)
-    if (F > P.obj) { lo = P.vmin; hi = P.sg0; br = 0; }
-    if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; br = 1; }
-    if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; br = 2; }
-    if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; br = 3; }
-    bool ustack = !(hi == P.sg0 || hi == P.sg1);
-    int plo = br >= 0 ? fixpos(lo) : 0, phi = br >= 0 ? max(fixpos(hi), plo) : 0;
-    stamp(4);
+    bool ustack = false;
+    int plo = 0, phi = 0;                                  // the bracket's sorted positions [plo, phi)
     int h = 1;                                             // heap index of (lo, hi) in the bracket's tree
-    const int* tr = G.tree + (max(br, 0) << G.depth);
-    const int tsz = br >= 0 ? (1 << G.depth) : 0;          // tabulated heap nodes [1, tsz)
-    int pmt = tsz > 1 ? tr[1] : 0;                         // ub(mid) of heap node h, loaded a level ahead
-
-    // ---- (iv) bisection (:250-309); Q2 / Q4 are resolved across dates by the finalize
-    double prev = F, prevU = prevU0;
+    const int* tr = G.tree;
+    int tsz = 0;                                           // tabulated heap nodes [1, tsz)
+    double prev = 0.0, prevU = 0.0;
     int nt = -1, it = 0;
     uint64_t mask = 0;
     double* sn = snaps + t * P.stride;
+    // (i)-(iii) from r0 = I(lower, fg] and the second slab nr (Q1, Q3)
+    auto bracket = [&](double r0, double nl, double nu, double nr) {
+        const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
+        if (F > P.obj) { lo = P.vmin; hi = P.sg0; br = 0; }
+        if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; br = 1; }
+        if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; br = 2; }
+        if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; br = 3; }
+        ustack = !(hi == P.sg0 || hi == P.sg1);
+        plo = br >= 0 ? fixpos(lo) : 0;
+        phi = br >= 0 ? max(fixpos(hi), plo) : 0;
+        tr = G.tree + (max(br, 0) << G.depth);
+        tsz = br >= 0 ? (1 << G.depth) : 0;
+        prev = F;
+        prevU = (nl == P.sg0) ? P.sg0 : P.fg;
+        stamp(4);
+    };
+    // one bisection level from a slab value (adjust_integral :214-248, Q4 mask)
+    auto level = [&](double mid, double val) {
+        const double slab_lower = ustack ? lo : mid;
+        const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
+        if (Fn != 0.0) mask |= (1ull << it);
+        ustack = Fn < P.obj;
+        prev = Fn;
+        prevU = mid;
+        return ustack;
+    };
     if constexpr (SWEEP) {
-        // levels of the subtree (depth Ds) whose in-order boundary list starts at Bl + o:
-        // heap node (level l, path m) is entry (2m + 1) 2^(Ds - 1 - l) - 1
-        auto descend = [&](const int* Bl, const double* Pv, int o, int Ds, double Plo, double Phi) {
-            int m = 0;
-            for (int l = 0; l < Ds && it < P.K && phi - plo > TCAP; ++l, ++it) {
+        // Passes share one code instance (register pressure): pass 0 covers (lower, sg1] with
+        // the fixed levels and brackets 0, 1, 3's subtrees; later passes one cell of the bracket.
+        const int M0 = (1 << G.d0) - 1;
+        int ps = G.fix[0], pe = G.fix[3], M = 3 * M0 + 3, buf = 0, npass = 0;
+        int* Bl = Bls;
+        double* Pv = Pvs;
+        const uint32_t* trw = G.trw0;
+        while (true) {
+            const double tot = sweep(ps, pe, Bl, Pv, M, trw);
+            if (npass < 3) stamp(npass == 0 ? 2 : 3 + 3 * npass);
+            nodes += pe - ps;
+            int o = 0, Ds = 0;
+            double Plo = 0.0, Phi = tot;
+            if (npass == 0) {
+                const double Pvmin = Pv[0], Psg0 = Pv[M0 + 1], Pfg = Pv[2 * M0 + 2];
+                const double r0 = Pfg;                     // (lower, fg]
+                const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+                const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+                bracket(r0, nl, nu, (nl == P.fg) ? tot - Pfg : Pfg - Psg0);   // (fg, sg1] or (sg0, fg]
+                if (br == 0) { o = 1; Ds = G.d0; Plo = Pvmin; Phi = Psg0; }
+                if (br == 1) { o = M0 + 2; Ds = G.d0; Plo = Psg0; Phi = Pfg; }
+                if (br == 3) { o = 2 * M0 + 3; Ds = G.d0; Plo = Pfg; Phi = tot; }
+            } else {
+                Ds = M == 0 ? 0 : 31 - __builtin_clz(M + 1);
+            }
+            // the subtree's levels from LDS: heap node (level l, path m) is entry (2m + 1) 2^(Ds - 1 - l) - 1
+            for (int l = 0, m = 0; l < Ds && it < P.K && phi - plo > TCAP; ++l, ++it) {
                 const double mid = (lo + hi) / 2;
                 if (tid == 0) sn[it] = mid;
                 if (nt < 0 && !(hi - lo > P.tol)) nt = it;
                 const int ii = o + ((2 * m + 1) << (Ds - 1 - l)) - 1;
                 const int pm = Bl[ii];
                 const double Pm = Pv[ii];
-                const double val = ustack ? Pm - Plo : Phi - Pm;
-                const double slab_lower = ustack ? lo : mid;
-                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
-                if (Fn != 0.0) mask |= (1ull << it);
-                ustack = Fn < P.obj;
-                if (ustack) { lo = mid; plo = pm; Plo = Pm; m = 2 * m + 1; }
-                else        { hi = mid; phi = pm; Phi = Pm; m = 2 * m; }
+                if (level(mid, ustack ? Pm - Plo : Phi - Pm)) { lo = mid; plo = pm; Plo = Pm; m = 2 * m + 1; }
+                else                                         { hi = mid; phi = pm; Phi = Pm; m = 2 * m; }
                 h = 2 * h + (ustack ? 1 : 0);
-                prev = Fn;
-                prevU = mid;
             }
-        };
-        if (br == 0) descend(Bls, Pvs, 1, G.d0, Pvmin, Psg0);
-        else if (br == 1) descend(Bls, Pvs, M0 + 2, G.d0, Psg0, Pfg);
-        else if (br == 3) descend(Bls, Pvs, 2 * M0 + 3, G.d0, Pfg, tot0);
-        int buf = 0;
+            if (npass < 3) stamp(npass == 0 ? 3 : 4 + 3 * npass);
+            ++npass;
+            if (!(it < P.K && phi - plo > TCAP && h < tsz)) break;
+            // next pass: the cell (lo, hi] with its subtree of depth Ds (tabulated heap nodes only)
+            const int nDs = min(G.dsweep, G.depth - (31 - __builtin_clz(h)));
+            M = (1 << nDs) - 1;
+            buf ^= 1;
+            Bl = Bls + buf * kSweepCap;
+            Pv = Pvs + buf * kSweepCap;
+            for (int k = tid; k < M; k += NT) {             // in-order entry k -> heap node
+                const int l = nDs - 1 - __builtin_ctz(k + 1), m = (k + 1) >> (nDs - l);
+                Bl[k] = tr[(h << l) + m];
+            }
+            ps = plo;
+            pe = phi;
+            trw = (h == 1 && br == 2) ? G.trw2 : nullptr;
+            __syncthreads();
+        }
+        // beyond the tabulated tree (ties pile up): one searched level at a time
         while (it < P.K && phi - plo > TCAP) {
-            const int lvl = 31 - __builtin_clz(h);
-            if (h < tsz) {                                 // one pass over the cell (lo, hi]
-                const int Ds = min(G.dsweep, G.depth - lvl);
-                const int M = (1 << Ds) - 1;
-                buf ^= 1;
-                int* Bl = Bls + buf * kSweepCap;
-                double* Pv = Pvs + buf * kSweepCap;
-                for (int k = tid; k < M; k += NT) {         // in-order entry k -> heap node
-                    const int l = Ds - 1 - __builtin_ctz(k + 1), m = (k + 1) >> (Ds - l);
-                    Bl[k] = tr[(h << l) + m];
-                }
-                __syncthreads();
-                const double tot = sweep(plo, phi, Bl, Pv, M, (h == 1 && br == 2) ? G.trw2 : nullptr);
-                nodes += phi - plo;
-                descend(Bl, Pv, 0, Ds, 0.0, tot);
-            } else {                                       // beyond the tabulated tree: one level
-                const double mid = (lo + hi) / 2;
-                if (tid == 0) sn[it] = mid;
-                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-                const int pm = sorted_ub(G.vs, plo, phi, mid);
-                const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
-                nodes += ustack ? pm - plo : phi - pm;
-                const double slab_lower = ustack ? lo : mid;
-                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
-                if (Fn != 0.0) mask |= (1ull << it);
-                ustack = Fn < P.obj;
-                if (ustack) { lo = mid; plo = pm; }
-                else        { hi = mid; phi = pm; }
-                prev = Fn;
-                prevU = mid;
-                ++it;
-            }
+            const double mid = (lo + hi) / 2;
+            if (tid == 0) sn[it] = mid;
+            if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+            const int pm = sorted_ub(G.vs, plo, phi, mid);
+            const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
+            nodes += ustack ? pm - plo : phi - pm;
+            if (level(mid, val)) { lo = mid; plo = pm; }
+            else                 { hi = mid; phi = pm; }
+            ++it;
         }
     } else {
-    for (; it < P.K && phi - plo > TCAP; ++it) {
-        const double mid = (lo + hi) / 2;
-        if (tid == 0) sn[it] = mid;
-        if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-        const bool tab = h < tsz;                          // tabulated; deeper: search (only if ties pile up)
-        const int pm = tab ? pmt : sorted_ub(G.vs, plo, phi, mid);
-        const bool ctab = 2 * h + 1 < tsz;                 // both children tabulated: fetch them now,
-        const int pl = ctab ? tr[2 * h] : 0;               // their latency hides behind this level's slab
-        const int pr = ctab ? tr[2 * h + 1] : 0;
-        const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
-        nodes += ustack ? pm - plo : phi - pm;
-        const double slab_lower = ustack ? lo : mid;
-        const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
-        if (Fn != 0.0) mask |= (1ull << it);
-        ustack = Fn < P.obj;
-        if (ustack) { lo = mid; plo = pm; }
-        else        { hi = mid; phi = pm; }
-        if (tab) h = 2 * h + (ustack ? 1 : 0);             // children: (lo, mid) = 2h, (mid, hi) = 2h + 1
-        pmt = ustack ? pr : pl;
-        if (it < 15) stamp(5 + it);
-        prev = Fn;
-        prevU = mid;
-    }
+        const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));   // (lower, fg]
+        stamp(2);
+        nodes += max(G.fix[2] - G.fix[0], 0);
+        const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+        stamp(3);
+        nodes += max(fixpos(nu) - fixpos(nl), 0);
+        bracket(r0, nl, nu, nr);
+        int pmt = tsz > 1 ? tr[1] : 0;                     // ub(mid) of heap node h, loaded a level ahead
+        for (; it < P.K && phi - plo > TCAP; ++it) {
+            const double mid = (lo + hi) / 2;
+            if (tid == 0) sn[it] = mid;
+            if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+            const bool tab = h < tsz;                      // tabulated; deeper: search (only if ties pile up)
+            const int pm = tab ? pmt : sorted_ub(G.vs, plo, phi, mid);
+            const bool ctab = 2 * h + 1 < tsz;             // both children tabulated: fetch them now,
+            const int pl = ctab ? tr[2 * h] : 0;           // their latency hides behind this level's slab
+            const int pr = ctab ? tr[2 * h + 1] : 0;
+            const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
+            nodes += ustack ? pm - plo : phi - pm;
+            if (level(mid, val)) { lo = mid; plo = pm; }
+            else                 { hi = mid; phi = pm; }
+            if (tab) h = 2 * h + (ustack ? 1 : 0);         // children: (lo, mid) = 2h, (mid, hi) = 2h + 1
+            pmt = ustack ? pr : pl;
+            if (it < 15) stamp(5 + it);
+        }
     }
 
     // ---- tail: the bracket's <= TCAP nodes -> LDS, wave 0 finishes the levels

@@ -18,4 +18,4 @@ for p in "${passes[@]}"; do
   i=$((i+1))
 done
 python3 tools/pmc_summary.py $out "$@" > $out/summary.txt
-grep -A20 "k_direct\|k_compact" $out/summary.txt | head -44
+grep -A20 "k_direct\|k_compact\|k_sorted" $out/summary.txt | head -44 || true

@@ -38,7 +38,7 @@ for k, d in sorted(summ.items()):
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {v:16.1f}")
-dom = {"prefix": "k_mass", "compact": "k_compact", "sorted": "k_sorted"}.get(strategy, "k_direct")
+dom = {"prefix": "k_mass", "compact": "k_compact", "sorted": "k_sorted", "sweep": "k_sorted"}.get(strategy, "k_direct")
 mass = [k for k in summ if re.search(rf"\b{dom}\b", k)]
 if mass:
     d = summ[mass[0]]

@@ -33,7 +33,7 @@ else:   # COMPACT / SORTED: 0 start, 1 tables, 2 slab1, 3 slab2, 4 bracket, 5+it
     lev = [i for i in range(5, 20) if (st[:, i] != 0).any()]
     cols = [0, 1, 2, 3, 4] + lev + [29, 31]
     names = ["tables", "slab1", "slab2", "bracket"] + [f"lev{i - 5}" for i in lev] + ["tailbuild", "tail"]
-if STRAT == "sorted":
+if STRAT in ("sorted", "sweep"):
     nodes = st[:, 28]
     print(f"nodes evaluated per date: mean {nodes.mean():.0f} p50 {np.median(nodes):.0f} max {nodes.max()} "
           f"(reachable {p.reach_nodes})")
