@@ -30,7 +30,7 @@ template <int COP, bool MSM, int PM, bool FUSED, int RPT>
 void launch_r(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
     hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED>), dim3((unsigned)L.T), dim3(NT),
-                       compact_lds_bytes(L.S.n, NT, L.G.nb), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st,
+                       compact_lds_bytes(L.S.n, NT, L.G.nb, kColgInRow<COP>), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st,
                        L.snaps, L.hdr);
 }
 

@@ -54,8 +54,18 @@ constexpr int kTailCap = 64 * kTailPerLane;         // bracket size that switche
 constexpr int kRowRec = 8;                          // doubles per LDS row record
 constexpr int kColRec = 2;                          // doubles per LDS column record (16 B: lanes at
                                                     // consecutive columns read conflict-free)
-constexpr int kCutFixed = 8;                        // int16 per row in the fixed-level cut table
+constexpr int kCutFixed = 8;                        // int16 per row in the fixed-level cut table (HBM)
+constexpr int kCutLds = 6;                          // int16 per row of its LDS copy (the 6 used columns)
 constexpr int kBucketsPerPoint = 4;                 // grid lookup buckets per grid point
+// LDS budget: <= 32 KB per workgroup at n = 256 so five dates share a CU (160 KB):
+// the generic path's column words (B_j, wc_j) live in the row records' unused
+// Plackett slots [2], [3] for the Student / Gaussian kernels, and the LDS cut
+// table keeps 6 of the HBM table's 8 columns.
+template <int COP>
+constexpr bool kColgInRow = COP != CVQ_PLACKETT;
+#ifndef CVQ_COMPACT_WAVES
+#define CVQ_COMPACT_WAVES 0                         // min waves per SIMD (0: compiler default)
+#endif
 #ifndef CVQ_COMPACT_ILP
 #define CVQ_COMPACT_ILP 2
 #endif
@@ -71,6 +81,11 @@ struct CompactGeom {
     const int16_t* bucket;    // [nb] largest j with x_j <= bx0 + b / binv (0 if none): a start guess
     double bx0, binv;         // bucket of a grid coordinate g: floor((g - bx0) * binv)
     int nb;
+    // [4][1 << cdepth] node counts of the bisection cells (heap node h of bracket b's tree at
+    // (b << cdepth) + h, 1 <= h < 2^cdepth; every depth-cdepth cell holds <= kTailCap nodes);
+    // nullptr: the levels reduce the bracket's node count on the device
+    const int* ccount;
+    int cdepth;
 };
 
 // ------------------------------------------------------------------ reductions
@@ -145,6 +160,23 @@ __device__ __forceinline__ void team_sum3(double a, double b, double c, double* 
     out[0] = s0;
     out[1] = s1;
     out[2] = s2;
+}
+
+// Workgroup sum of one value, identical in every thread (fixed order), one barrier;
+// shares team_sum3's slots (parity alternates the half used).
+template <int NT>
+__device__ __forceinline__ double team_sum1(double a, double* red, int& parity) {
+    a = wave_sum(a);
+    if constexpr (NT == 64) return a;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double* rr = red + parity * (3 * (NT / 64));
+    parity ^= 1;
+    if (lane == 0) rr[wave] = a;
+    __syncthreads();
+    double s = rr[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) s += rr[w];
+    return s;
 }
 
 // count_le(sx, g, klo, khi) -- the largest j in [klo, khi] with x_j <= g, else klo
@@ -341,8 +373,13 @@ __device__ __forceinline__ void fused_finalize(const SolveConst& P, Header* hdr,
 // Thread tid owns rows tid + NT k (k < RPT, RPT = ceil(n / NT)); NT = 64 makes the
 // whole solve one wavefront: no barriers, no LDS round trips in the reductions.
 // FUSED: evaluate the date's tables here; else read k_tables' tA / tB.
+#if CVQ_COMPACT_WAVES > 0
+#define CVQ_COMPACT_BOUNDS(NT) __launch_bounds__(NT, CVQ_COMPACT_WAVES)
+#else
+#define CVQ_COMPACT_BOUNDS(NT) __launch_bounds__(NT)
+#endif
 template <int COP, bool MSM, int NT, int RPT, int PM, bool FUSED>
-__global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, CompactGeom G, const double* __restrict__ a,
+__global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, CompactGeom G, const double* __restrict__ a,
                                                 const double* __restrict__ tA, const double* __restrict__ tB,
                                                 const double* __restrict__ pi, double* __restrict__ stamps_out,
                                                 double* __restrict__ snaps, Header* hdr) {
@@ -350,14 +387,16 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
     const long long t = blockIdx.x;
     double* col = lds;                              // [n][kColRec]: z_j, B'_j = B_j wc_j
-    double* colg = col + kColRec * n;               // [n][2]: B_j, wc_j (generic path)
-    double* rowr = colg + 2 * n;                    // [n][kRowRec]: c0 c1 c2 c3 scale | z0 B0 wr
+    // [n][2]: B_j, wc_j (generic path), stride cgs; Student / Gaussian: row record slots [2], [3]
+    constexpr int cgs = kColgInRow<COP> ? kRowRec : 2;
+    double* rowr = col + kColRec * n + (kColgInRow<COP> ? 0 : 2 * n);   // [n][kRowRec]: c0 c1 c2 c3 scale | z0 B0 wr
+    double* colg = kColgInRow<COP> ? rowr + 2 : col + kColRec * n;
     double* sx = rowr + kRowRec * n;                // [n] grid
     double2* tail = (double2*)(sx + n);             // [kTailCap] tail nodes: (v*, value)
     double* red = (double*)(tail + kTailCap);       // [2][3][NT / 64] reduction slots
     int* wtot = (int*)(red + 6 * (NT / 64));        // [NT / 64] scan slots (padded to 16 B)
-    int16_t* cfx = (int16_t*)(wtot + kWtotInts<NT>);   // [n][kCutFixed] fixed-level cuts (16-B aligned)
-    int16_t* bk = cfx + (size_t)kCutFixed * n;      // [nb] grid lookup buckets
+    int16_t* cfx = (int16_t*)(wtot + kWtotInts<NT>);   // [n][kCutLds] fixed-level cuts
+    int16_t* bk = cfx + (size_t)kCutLds * n;        // [nb] grid lookup buckets
     __shared__ int flags;                           // bit 0: non-finite table entry, bit 1: pi not rank 1
 
     unsigned long long* stamps = stamps_out ? (unsigned long long*)stamps_out + t * 32 : nullptr;
@@ -373,7 +412,9 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
         row[k] = tid + NT * k;
         own[k] = row[k] < n;
     }
-    for (int w = tid; w < kCutFixed * n / 8; w += NT) ((int4*)cfx)[w] = ((const int4*)G.cutfix)[w];
+    static_assert(kCutLds % 2 == 0 && kCutFixed % 2 == 0, "cut rows copied as int pairs");
+    for (int w = tid; w < (kCutLds / 2) * n; w += NT)
+        ((int*)cfx)[w] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
     for (int b = tid; b < G.nb; b += NT) bk[b] = G.bucket[b];
     for (int i = tid; i < n; i += NT) sx[i] = S.x[i];
     if (tid == 0) flags = 0;
@@ -408,10 +449,10 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
         if (!isfinite(A[0]) || !isfinite(B[0]) || !isfinite(A[1]) || !isfinite(B[1])) bad |= 1;
         col[kColRec * i] = A[1];
         col[kColRec * i + 1] = B[1] * wc;
-        colg[2 * i] = B[1];
-        colg[2 * i + 1] = wc;
         double* rr = rowr + kRowRec * i;
         fast_row_consts<COP>(S, A[0], B[0], wr, rr);
+        colg[cgs * i] = B[1];                                      // after the row constants: may share rr[2..3]
+        colg[cgs * i + 1] = wc;
         rr[5] = A[0];
         rr[6] = B[0];
         rr[7] = wr;
@@ -439,7 +480,7 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
         if (!fast) {
             double acc = 0.0;
             for (int j = j0; j <= j1; ++j)
-                acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + 2 * j, rr, j, rank1,
+                acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + cgs * j, rr, j, rank1,
                                               pit);
             return acc;
         }
@@ -482,7 +523,7 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
         team_sum3<NT>(part, (double)ns, (double)nb, red, parity, sums);
     };
     auto fixcut = [&](int k, double v) {                         // one of the solve's fixed levels
-        const int16_t* c = cfx + (size_t)(own[k] ? row[k] : 0) * kCutFixed;
+        const int16_t* c = cfx + (size_t)(own[k] ? row[k] : 0) * kCutLds;
         return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
              : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : v == P.vmax ? c[kCutVmax]
              : grid_count(sx, bk, G, (v - lev[k]) / S.w0, 0, n - 1);
@@ -497,8 +538,8 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
         for (int k = 0; k < RPT; ++k) {
             if (!own[k]) continue;
             const int r1 = row[k], r2 = n - 1 - row[k];
-            const int16_t* c1 = cfx + (size_t)r1 * kCutFixed;
-            const int16_t* c2 = cfx + (size_t)r2 * kCutFixed;
+            const int16_t* c1 = cfx + (size_t)r1 * kCutLds;
+            const int16_t* c2 = cfx + (size_t)r2 * kCutLds;
             auto cut = [&](const int16_t* c, double v) {
                 return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
                      : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : c[kCutVmax];
@@ -509,7 +550,7 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
             if (m1 > a1) part += range_sum(r1, a1 + 1, m1);
             if (b2 > m2) part += range_sum(r2, m2 + 1, b2);
         }
-        team_sum3<NT>(part, 0.0, 0.0, red, parity, sums);
+        sums[0] = team_sum1<NT>(part, red, parity);
     };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
@@ -524,10 +565,11 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);
     double lo = __builtin_nan(""), hi = __builtin_nan("");
-    if (F > P.obj) { lo = P.vmin; hi = P.sg0; }
-    if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; }
-    if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; }
-    if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; }
+    int bsel = -1;                                               // bracket: the host cell tables' index
+    if (F > P.obj) { lo = P.vmin; hi = P.sg0; bsel = 0; }
+    if (F < P.obj && nu == P.fg) { lo = P.sg0; hi = P.fg; bsel = 1; }
+    if (F < P.obj && nu == P.sg1) { lo = P.sg1; hi = P.vmax; bsel = 2; }
+    if (F > P.obj && nu == P.sg1) { lo = P.fg; hi = P.sg1; bsel = 3; }
     bool ustack = !(hi == P.sg0 || hi == P.sg1);
     int kLo[RPT], kHi[RPT];
 #pragma unroll
@@ -545,11 +587,20 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     // the tail runs on wave 0; its lane 0 owns the header (rotating the tail wave
     // by date, to spread the tails of a CU's dates over its SIMDs, measured slower)
     const int leader = 0;
-    int nbr_next = 1 << 30;                                      // bracket nodes after the level
+    // bracket nodes: the host's cell table (heap node hc of bracket bsel's tree), else
+    // reduced with the level's sum; a NaN bracket (Q3) holds none
+    const bool tabc = G.ccount != nullptr;
+    const int* cc = tabc ? G.ccount + ((size_t)max(bsel, 0) << G.cdepth) : nullptr;
+    const int hend = tabc ? 1 << G.cdepth : 0;
+    int hc = 1;
+    int nbr_next = !tabc ? 1 << 30 : (bsel < 0 || hc >= hend) ? 0 : cc[hc];
     for (; it < P.K && nbr_next > kTailCap; ++it) {
         const double mid = (lo + hi) / 2;
         if (tid == 0) sn[it] = mid;
         if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+        // the children's counts, loaded while the level runs (depth cdepth: all <= kTailCap)
+        const int c_lo = (tabc && 2 * hc < hend) ? cc[2 * hc] : 0;
+        const int c_hi = (tabc && 2 * hc + 1 < hend) ? cc[2 * hc + 1] : 0;
         int kM[RPT];
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
@@ -561,22 +612,37 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
             ka[k] = ustack ? kLo[k] : kM[k];
             kb[k] = ustack ? kM[k] : kHi[k];
         }
-        level_sums(ka, kb, kLo, kHi);
-        const double val = sums[0];
-        const int Ns = (int)sums[1], Nbr = (int)sums[2];
-        const int Nlow = ustack ? Ns : Nbr - Ns;                 // nodes of (lo, mid]
+        double val;
+        int Nlow = 0, Nbr = 0;
+        if (tabc) {
+            double part = 0.0;
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                const int len = own[k] ? max(kb[k] - ka[k], 0) : 0;
+                if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
+            }
+            val = team_sum1<NT>(part, red, parity);
+        } else {
+            level_sums(ka, kb, kLo, kHi);
+            val = sums[0];
+            const int Ns = (int)sums[1];
+            Nbr = (int)sums[2];
+            Nlow = ustack ? Ns : Nbr - Ns;                       // nodes of (lo, mid]
+        }
         const double slab_lower = ustack ? lo : mid;
         const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
         if (Fn != 0.0) mask |= (1ull << it);
         ustack = Fn < P.obj;
         if (ustack) {
             lo = mid;
-            nbr_next = Nbr - Nlow;
+            nbr_next = tabc ? c_hi : Nbr - Nlow;
+            hc = 2 * hc + 1;
 #pragma unroll
             for (int k = 0; k < RPT; ++k) kLo[k] = kM[k];
         } else {
             hi = mid;
-            nbr_next = Nlow;
+            nbr_next = tabc ? c_lo : Nlow;
+            hc = 2 * hc;
 #pragma unroll
             for (int k = 0; k < RPT; ++k) kHi[k] = kM[k];
         }
@@ -655,11 +721,11 @@ __global__ __launch_bounds__(NT) void k_compact(StaticDev S, SolveConst P, Compa
     fused_finalize<NT>(P, hdr, snaps, (long long)gridDim.x);
 }
 
-// LDS bytes of one k_compact workgroup
-inline size_t compact_lds_bytes(int n, int nt, int nb) {
-    return sizeof(double) * ((size_t)(kColRec + 2 + kRowRec + 1) * n) + sizeof(double2) * kTailCap +
+// LDS bytes of one k_compact workgroup (cfg 2, n = 256, Student: 31,952 B)
+inline size_t compact_lds_bytes(int n, int nt, int nb, bool colg_in_row) {
+    return sizeof(double) * ((size_t)(kColRec + (colg_in_row ? 0 : 2) + kRowRec + 1) * n) + sizeof(double2) * kTailCap +
            sizeof(double) * 6 * (nt / 64) + sizeof(int) * (((nt / 64) + 3) & ~3) +
-           sizeof(int16_t) * ((size_t)kCutFixed * n + nb);
+           sizeof(int16_t) * ((size_t)kCutLds * n + nb);
 }
 
 }  // namespace cvq

@@ -155,6 +155,9 @@ struct cvq_plan {
     int16_t* d_cutfix = nullptr; // [n][kCutFixed]
     double cut_key[6] = {0, 0, 0, 0, 0, 0};
     bool cut_valid = false;
+    std::vector<double> hvc;     // every v*(r, j >= 1), sorted (the bisection cells' node counts)
+    int* d_ccount = nullptr;     // [4][1 << ccount_depth] cell node counts (nullptr: counted on device)
+    int ccount_depth = -1;
     // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
     // ub() of the fixed levels and the bisection trees for the cached solve arguments
     std::vector<double> hvs;
@@ -668,7 +671,46 @@ void build_buckets(const std::vector<double>& x, std::vector<int16_t>& bk, doubl
     }
 }
 
-// Fixed-level cut table for the cached solve arguments.
+// COMPACT: node counts of the bisection cells -- heap node h of bracket b's tree holds
+// #{(r, j >= 1): lo_h < v*(r, j) <= hi_h}, with the device's mids (lo + hi) / 2 -- for
+// every depth above the first one whose cells all hold <= kTailCap nodes.  The kernel
+// enters its one-wave tail from this table instead of reducing bracket node counts at
+// every level.  depth = -1: no such depth <= kCompactMaxDepth (the kernel counts).
+constexpr int kCompactMaxDepth = 16;
+void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, std::vector<int>& cc, int* depth) {
+    const double br[4][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.sg1, P.vmax}, {P.fg, P.sg1}};   // k_compact's brackets
+    std::vector<std::vector<int>> cnt;                      // cnt[d][(b << d) + k]: depth-d cell k of bracket b
+    std::vector<double> lo(4), hi(4);
+    for (int b = 0; b < 4; ++b) { lo[b] = br[b][0]; hi[b] = br[b][1]; }
+    *depth = -1;
+    for (int d = 0; d <= std::min(kCompactMaxDepth, std::max(P.K, 0)); ++d) {
+        std::vector<int> c(lo.size());
+        bool small = true;
+        for (size_t e = 0; e < lo.size(); ++e) {
+            c[e] = std::max(host_ub(vs, hi[e]) - host_ub(vs, lo[e]), 0);
+            small = small && c[e] <= kTailCap;
+        }
+        if (small) { *depth = d; break; }
+        cnt.push_back(c);
+        std::vector<double> l2(2 * lo.size()), h2(2 * lo.size());
+        for (size_t e = 0; e < lo.size(); ++e) {            // children 2k (lower half), 2k + 1 (upper half)
+            const double mid = (lo[e] + hi[e]) / 2;
+            l2[2 * e] = lo[e]; h2[2 * e] = mid;
+            l2[2 * e + 1] = mid; h2[2 * e + 1] = hi[e];
+        }
+        lo.swap(l2);
+        hi.swap(h2);
+    }
+    cc.clear();
+    if (*depth < 0) return;
+    const int D = *depth;
+    cc.assign((size_t)4 << D, 0);
+    for (int d = 0; d < D; ++d)
+        for (int b = 0; b < 4; ++b)
+            for (int k = 0; k < (1 << d); ++k) cc[((size_t)b << D) + (1 << d) + k] = cnt[d][((size_t)b << d) + k];
+}
+
+// Fixed-level cut table (and the bisection cells' node counts) for the cached solve arguments.
 int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
     if (p->cut_valid && std::memcmp(key, p->cut_key, sizeof key) == 0) return CVQ_OK;
@@ -681,6 +723,15 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     p->cut_valid = false;
     if (!p->d_cutfix) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cutfix, h.size() * sizeof(int16_t)));
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cutfix, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
+    std::vector<int> cc;
+    build_cell_counts(p->hvc, P, cc, &p->ccount_depth);
+    static const bool no_cc = getenv("CVQ_COMPACT_COUNT") && atoi(getenv("CVQ_COMPACT_COUNT")) != 0;   // A/B switch
+    if (no_cc) p->ccount_depth = -1;
+    if (p->ccount_depth >= 0) {
+        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));   // the previous table may still be read
+        if (int rc = dev_alloc(&p->d_ccount, cc.size())) return rc;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_ccount, cc.data(), cc.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
+    }
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     std::memcpy(p->cut_key, key, sizeof key);
     p->cut_valid = true;
@@ -741,7 +792,8 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         double* st = nullptr;
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         if (dbg_stamps) st = (double*)p->d_stamps;
-        const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb};
+        const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
+                            p->ccount_depth >= 0 ? p->d_ccount : nullptr, p->ccount_depth};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr);
     }
@@ -1139,6 +1191,11 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     if (p->strategy == CVQ_STRATEGY_COMPACT) {         // exact level thresholds + grid lookup buckets
         std::vector<double> vs;
         build_vstar(p->hx, S.w0, S.w1, vs);
+        p->hvc.clear();
+        p->hvc.reserve((size_t)n * (n - 1));
+        for (int r = 0; r < n; ++r)
+            for (int j = 1; j < n; ++j) p->hvc.push_back(vs[(size_t)r * n + j]);   // COMPACT's nodes: j >= 1 (Q9)
+        std::sort(p->hvc.begin(), p->hvc.end());
         std::vector<int16_t> bk;
         build_buckets(p->hx, bk, &p->bx0, &p->binv);
         p->nb = (int)bk.size();
@@ -1163,7 +1220,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);

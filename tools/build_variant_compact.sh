@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build a libcvq.so variant with extra -D flags on the COMPACT translation unit (CPU container).
+# usage: tools/build_variant_compact.sh <name> <flags...>   -> build_variants/<name>/libcvq.so
+set -e
+name=$1; shift
+cd "$(dirname "$0")/../copula-msm-and-copula-garch-var_amd"
+out=../build_variants/$name
+mkdir -p $out
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function "$@" \
+    -c csrc/cvq_compact.hip -o $out/cvq_compact.o -Rpass-analysis=kernel-resource-usage 2> $out/resource.txt
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libcvq.so build/cvq_plan.o build/cvq_forecast.o \
+    $out/cvq_compact.o build/cvq_sorted.o
