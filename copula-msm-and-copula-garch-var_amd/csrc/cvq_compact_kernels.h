@@ -397,7 +397,6 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     int* wtot = (int*)(red + 6 * (NT / 64));        // [NT / 64] scan slots (padded to 16 B)
     int16_t* cfx = (int16_t*)(wtot + kWtotInts<NT>);   // [n][kCutLds] fixed-level cuts
     int16_t* bk = cfx + (size_t)kCutLds * n;        // [nb] grid lookup buckets
-    __shared__ int flags;                           // bit 0: non-finite table entry, bit 1: pi not rank 1
 
     unsigned long long* stamps = stamps_out ? (unsigned long long*)stamps_out + t * 32 : nullptr;
     auto stamp = [&](int idx) {                     // diagnostic only (never in a timed run)
@@ -412,13 +411,22 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         row[k] = tid + NT * k;
         own[k] = row[k] < n;
     }
+    // static LDS images (grid, lookup buckets, fixed-level cuts): every load issued here,
+    // the stores after the tables phase, so their latency hides behind the tables' own
+    // loads (n <= NT RPT, nb = kBucketsPerPoint n; clamped indices stay in bounds)
     static_assert(kCutLds % 2 == 0 && kCutFixed % 2 == 0, "cut rows copied as int pairs");
-    for (int w = tid; w < (kCutLds / 2) * n; w += NT)
-        ((int*)cfx)[w] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
-    for (int b = tid; b < G.nb; b += NT) bk[b] = G.bucket[b];
-    for (int i = tid; i < n; i += NT) sx[i] = S.x[i];
-    if (tid == 0) flags = 0;
-    __syncthreads();
+    constexpr int kBkPer = kBucketsPerPoint * RPT, kCutPer = (kCutLds / 2) * RPT;
+    double xv[RPT];
+    int bv[kBkPer], cv[kCutPer];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) xv[k] = S.x[min(tid + NT * k, n - 1)];
+#pragma unroll
+    for (int k = 0; k < kBkPer; ++k) bv[k] = G.bucket[min(tid + NT * k, G.nb - 1)];
+#pragma unroll
+    for (int k = 0; k < kCutPer; ++k) {
+        const int w = min(tid + NT * k, (kCutLds / 2) * n - 1);
+        cv[k] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
+    }
 
     // ---- tables: index i -> row record i (axis 0) and column record i (axis 1)
     const int q = MSM ? S.q : 1;
@@ -438,9 +446,25 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         double wr, wc;                                             // row / column weight factors
         if constexpr (MSM) {
             wr = wc = 0.0;
-            for (int b = 0; b < q; ++b) {
-                wr = fma(fb[b], S.F[(size_t)b * n + i], wr);
-                wc = fma(fb[q + b], S.F[((size_t)q + b) * n + i], wc);
+            if (q <= kQUnroll) {                                   // every load issued before the chains
+                double fr[kQUnroll], fc[kQUnroll];
+#pragma unroll
+                for (int b = 0; b < kQUnroll; ++b) {
+                    const int bb = min(b, q - 1);
+                    fr[b] = S.F[(size_t)bb * n + i];
+                    fc[b] = S.F[((size_t)q + bb) * n + i];
+                }
+#pragma unroll
+                for (int b = 0; b < kQUnroll; ++b) {
+                    const int bb = min(b, q - 1);
+                    wr = b < q ? fma(fb[bb], fr[b], wr) : wr;
+                    wc = b < q ? fma(fb[q + bb], fc[b], wc) : wc;
+                }
+            } else {
+                for (int b = 0; b < q; ++b) {
+                    wr = fma(fb[b], S.F[(size_t)b * n + i], wr);
+                    wc = fma(fb[q + b], S.F[((size_t)q + b) * n + i], wc);
+                }
             }
         } else {
             wr = S.F[i];
@@ -462,12 +486,21 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         for (int l = tid; l < S.Q; l += NT)
             if (!(pit[l] == fb[l / q] * fb[q + l % q])) bad |= 2;
     }
-    if (bad) atomicOr(&flags, bad);
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+        if (tid + NT * k < n) sx[tid + NT * k] = xv[k];
+#pragma unroll
+    for (int k = 0; k < kBkPer; ++k)
+        if (tid + NT * k < G.nb) bk[tid + NT * k] = (int16_t)bv[k];
+#pragma unroll
+    for (int k = 0; k < kCutPer; ++k)
+        if (tid + NT * k < (kCutLds / 2) * n) ((int*)cfx)[tid + NT * k] = cv[k];
+    // MSM: only bit 1 (pi not rank 1) decides the path; GARCH / UKF: only bit 0 (a
+    // non-finite table entry, whose pi is rank 1 by construction)
+    const bool flag = __syncthreads_or(MSM ? (bad & 2) : (bad & 1)) != 0;
     stamp(1);
-    const int fl = flags;
-    const bool rank1 = !(fl & 2);
-    const bool fast = rank1 && (MSM || !(fl & 1));
+    const bool rank1 = !(MSM && flag);
+    const bool fast = rank1 && (MSM || !flag);
     double lev[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) lev[k] = sx[own[k] ? row[k] : 0] * S.w1;   // integration_algo.py:20 (2-D)

@@ -39,6 +39,9 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // Wave-wide sum, identical (bitwise) in every lane: symmetric DPP exchanges within
 // rows of 16 (xor 1, xor 2, half-mirror, mirror), then the four row sums combined
 // in a fixed order.  No LDS traffic.
+// unrolled vol-state loops (MSM q = k + 1 <= 8: k <= 7) issue their table loads together
+constexpr int kQUnroll = 8;
+
 __device__ __forceinline__ double wave_sum(double v) {
 #ifdef CVQ_SHFL_REDUCE
 #pragma unroll
@@ -80,8 +83,18 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
     if (MSM) {
         const double* f = a + td * S.q;
         const double* ph = S.phi + (size_t)d * S.q * S.n + i;
-        double acc = f[0] * ph[0];
-        for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
+        double acc;
+        if (S.q <= kQUnroll) {                                   // every load issued before the sum
+            double pv[kQUnroll];
+#pragma unroll
+            for (int s = 0; s < kQUnroll; ++s) pv[s] = ph[(size_t)min(s, S.q - 1) * S.n];
+            acc = f[0] * pv[0];
+#pragma unroll
+            for (int s = 1; s < kQUnroll; ++s) acc = s < S.q ? acc + f[min(s, S.q - 1)] * pv[s] : acc;
+        } else {
+            acc = f[0] * ph[0];
+            for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
+        }
         *u_out = acc;                                            // msm_integration_function.py:34-36
         *pdf_out = 1.0;
     } else {
