@@ -112,6 +112,8 @@ def main():
         d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
         d_b, b_ptr = None, None
     args = engine.solve_args(ptf_mean)
+    fast_ok = c.model == "msm" and bool(np.array_equal(                # the kernel's own rank-1 test, on the host
+        ipt[1], (ipt[0][:, 0, :, None] * ipt[0][:, 1, None, :]).reshape(ipt[1].shape))) if c.dim == 2 else False
     # `inflight` batches in flight: plan i (its own HIP stream, scratch and output)
     # solves steps i, i + inflight, ...  Consecutive batches are independent, so
     # the next one fills the CUs that the current one's last workgroups leave idle.
@@ -135,7 +137,9 @@ def main():
     def step_fn(i):
         k = i % nf
         with torch.cuda.stream(streams[k]):
-            plans[k].set_dates_device(per, d_a.data_ptr(), b_ptr)     # forces tables recompute
+            # pi = outer product of the per-asset forecasts (compute_forecast_combinations), so the
+            # fast path is asserted (a violating date would fail the solve status check below)
+            plans[k].set_dates_device(per, d_a.data_ptr(), b_ptr, fast=fast_ok)   # forces tables recompute
             if world == 1:
                 plans[k].solve_device(args, vars_[k].data_ptr())
             else:
@@ -271,7 +275,7 @@ def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):
         k = i % nf
         with torch.cuda.stream(streams[k]):
             mts[k].run(r_dev, streams[k].cuda_stream)
-            plans[k].set_dates_device(per, *ptrs(mts[k]))
+            plans[k].set_dates_device(per, *ptrs(mts[k]), fast=c.model == "msm")   # cvq_msm_tables: rank-1 pi
             plans[k].solve_device(args, vars_[k].data_ptr())
 
     for i in range(a.warmup):

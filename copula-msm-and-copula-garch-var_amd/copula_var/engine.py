@@ -136,12 +136,17 @@ class QuadraturePlan:
             N.check(N.lib().cvq_set_dates(self._h, T, N.ptr(a), None, N.MEM_HOST), "cvq_set_dates")
         self.T = int(T)
 
-    def set_dates_device(self, T: int, a_ptr: int, b_ptr: Optional[int] = None) -> None:
+    def set_dates_device(self, T: int, a_ptr: int, b_ptr: Optional[int] = None, fast: bool = False) -> None:
         """Per-date inputs already resident in device memory (e.g. torch tensors' data_ptr()).
         They are read in place by the following launches (no copy): keep them alive and
-        unchanged until the next set_dates."""
+        unchanged until the next set_dates.  fast=True asserts that every date takes
+        COMPACT's fast node path (MSM: pi_t is the outer product of the per-asset
+        forecasts, as the reference and cvq_msm_tables build it; GARCH/UKF: finite
+        marginal tables) -- cvq_set_fast_hint; a violating date fails the solve."""
         N.check(N.lib().cvq_set_dates(self._h, int(T), C.c_void_p(a_ptr), C.c_void_p(b_ptr or 0), N.MEM_DEVICE),
                 "cvq_set_dates")
+        if fast:
+            N.check(N.lib().cvq_set_fast_hint(self._h, 1), "cvq_set_fast_hint")
         self.T = int(T)
 
     # ------------------------------------------------------------ quadrature

@@ -2,6 +2,8 @@
 // unit: its template instances compile in parallel with cvq_plan.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #define CVQ_NO_PLAN_KERNELS
 
 #include "cvq_common.h"
@@ -23,15 +25,23 @@ struct CompactLaunch {
     const double *a, *tA, *tB, *pi;
     double *st, *snaps;
     Header* hdr;
+    int* defer;
     bool fused;
+    bool generic;                // launch the deferred-date (generic path) kernel
 };
+
+// deferred (generic-path) dates: a small grid loops over them
+constexpr long long kGenericGrid = 512;
 
 template <int COP, bool MSM, int PM, bool FUSED, int RPT>
 void launch_r(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
-    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED>), dim3((unsigned)L.T), dim3(NT),
-                       compact_lds_bytes(L.S.n, NT, L.G.nb, kColgInRow<COP>), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st,
-                       L.snaps, L.hdr);
+    const size_t lds = compact_lds_bytes(L.S.n, NT, L.G.nb, kColgInRow<COP>);
+    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, false>), dim3((unsigned)L.T), dim3(NT), lds, L.stream,
+                       L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.generic ? L.defer : nullptr, L.T);
+    if (!L.generic) return;
+    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, true>), dim3((unsigned)std::min(L.T, kGenericGrid)),
+                       dim3(NT), lds, L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.defer, L.T);
 }
 
 // rows per thread: ceil(n / NT) rounded up to 1, 2, 4 or 8 (n <= 8 NT)
@@ -71,8 +81,8 @@ int compact_max_n() { return 8 * CVQ_COMPACT_NT; }
 
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
-                   double* snaps, Header* hdr) {
-    const CompactLaunch L{S, P, G, T, stream, a, tA, tB, pi, st, snaps, hdr, fused};
+                   double* snaps, Header* hdr, int* defer, bool generic) {
+    const CompactLaunch L{S, P, G, T, stream, a, tA, tB, pi, st, snaps, hdr, defer, fused, generic};
     switch (S.copula) {
         case CVQ_GAUSSIAN: launch_c<CVQ_GAUSSIAN>(L); break;
         case CVQ_STUDENT: launch_c<CVQ_STUDENT>(L); break;

@@ -378,14 +378,22 @@ __device__ __forceinline__ void fused_finalize(const SolveConst& P, Header* hdr,
 #else
 #define CVQ_COMPACT_BOUNDS(NT) __launch_bounds__(NT)
 #endif
-template <int COP, bool MSM, int NT, int RPT, int PM, bool FUSED>
-__global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, CompactGeom G, const double* __restrict__ a,
-                                                const double* __restrict__ tA, const double* __restrict__ tB,
-                                                const double* __restrict__ pi, double* __restrict__ stamps_out,
-                                                double* __restrict__ snaps, Header* hdr) {
+// One date's solve by the whole workgroup: snapshots + this date's header bits.  GEN =
+// false compiles the fast node path only (63 instead of 107 VGPRs at cfg 2: five
+// workgroups per CU instead of four, +8.5%); a date that needs the generic path (pi not
+// rank 1, or a non-finite GARCH / UKF table entry) is appended to defer[2 ..] (count in
+// defer[0]) and left to the GEN = true kernel.  defer == nullptr: the caller asserted
+// that no date needs the generic path (cvq_set_fast_hint, or the host's proof in
+// cvq_set_dates) and no generic kernel follows -- such a date sets error bit 4 of the
+// header instead (the solve fails with CVQ_ERR_NUMERIC).  Returns true when deferred.
+template <int COP, bool MSM, int NT, int RPT, int PM, bool FUSED, bool GEN>
+__device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveConst& P, const CompactGeom& G,
+                                             const double* __restrict__ a, const double* __restrict__ tA,
+                                             const double* __restrict__ tB, const double* __restrict__ pi,
+                                             double* __restrict__ stamps_out, double* __restrict__ snaps, Header* hdr,
+                                             int* defer, const long long t) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
-    const long long t = blockIdx.x;
     double* col = lds;                              // [n][kColRec]: z_j, B'_j = B_j wc_j
     // [n][2]: B_j, wc_j (generic path), stride cgs; Student / Gaussian: row record slots [2], [3]
     constexpr int cgs = kColgInRow<COP> ? kRowRec : 2;
@@ -501,6 +509,15 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     stamp(1);
     const bool rank1 = !(MSM && flag);
     const bool fast = rank1 && (MSM || !flag);
+    if constexpr (!GEN) {
+        if (!fast) {                                             // uniform: the whole workgroup leaves
+            if (tid == 0) {
+                if (defer) defer[2 + atomicAdd(&defer[0], 1)] = (int)t;
+                else atomicOr(&hdr->error, 4);
+            }
+            return true;
+        }
+    }
     double lev[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) lev[k] = sx[own[k] ? row[k] : 0] * S.w1;   // integration_algo.py:20 (2-D)
@@ -509,15 +526,15 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     // sum of row rr's nodes j in [j0, j1] (fast path: row scale included, kIlp
     // independent chains; generic: node values)
     auto range_sum = [&](int rr, int j0, int j1) -> double {
-#ifndef CVQ_COMPACT_NOGENERIC
-        if (!fast) {
-            double acc = 0.0;
-            for (int j = j0; j <= j1; ++j)
-                acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + cgs * j, rr, j, rank1,
-                                              pit);
-            return acc;
+        if constexpr (GEN) {
+            if (!fast) {
+                double acc = 0.0;
+                for (int j = j0; j <= j1; ++j)
+                    acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + cgs * j, rr, j,
+                                                  rank1, pit);
+                return acc;
+            }
         }
-#endif
         const FastRow fr = load_fast_row<COP>(rowr + kRowRec * rr);
         constexpr int IL = (COP == CVQ_STUDENT && PM == 0) ? 1 : kIlp;   // general pow: register bound
         double acc[IL];
@@ -736,22 +753,65 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     stamp(31);
     if (stamps && tid == 0) stamps[26] = __builtin_amdgcn_s_memrealtime();
 
-    __shared__ int last;
     if (tid == leader) {
         sn[P.K] = (lo + hi) / 2;
         if (nt < 0 && !(hi - lo > P.tol)) nt = P.K;
         if (nt < 0) atomicOr(&hdr->error, 1);
         else atomicMax(&hdr->iters, nt);
         atomicOr((unsigned long long*)&hdr->nonzero, (unsigned long long)mask);
-        if (P.fin_var) {
-            __threadfence();                             // release: this date's snapshots + header bits
+    }
+    return false;
+}
+
+// The solve over T dates: GEN = false, one workgroup per date (grid T); GEN = true, a
+// small grid working through the dates the fast kernel deferred (none: every workgroup
+// leaves at once).  Fused finalize (P.fin_var) by the last workgroup of the launch that
+// completes the solve: the fast kernel when it deferred nothing, else the generic one.
+// defer[0] = deferred count, defer[1] = the generic kernel's ticket; both reset there.
+template <int COP, bool MSM, int NT, int RPT, int PM, bool FUSED, bool GEN>
+__global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, CompactGeom G, const double* __restrict__ a,
+                                                const double* __restrict__ tA, const double* __restrict__ tB,
+                                                const double* __restrict__ pi, double* __restrict__ stamps_out,
+                                                double* __restrict__ snaps, Header* hdr, int* defer, long long T) {
+    const int tid = threadIdx.x;
+    __shared__ int last;
+    if constexpr (!GEN) {
+        compact_date<COP, MSM, NT, RPT, PM, FUSED, false>(S, P, G, a, tA, tB, pi, stamps_out, snaps, hdr, defer,
+                                                          (long long)blockIdx.x);
+        if (!P.fin_var) return;
+        if (tid == 0) {
+            __threadfence();                             // release: this date's snapshots + header bits / deferral
             last = atomicAdd(&P.fin_err[3], 1) == (int)gridDim.x - 1;
         }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        if (!defer || __hip_atomic_load(&defer[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            fused_finalize<NT>(P, hdr, snaps, T);
+        } else if (tid == 0) {
+            P.fin_err[3] = 0;                            // the generic kernel finalizes
+        }
+    } else {
+        const int cnt = __hip_atomic_load(&defer[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
+            const long long t = defer[2 + k];
+            compact_date<COP, MSM, NT, RPT, PM, FUSED, true>(S, P, G, a, tA, tB, pi, stamps_out, snaps, hdr, defer, t);
+            __syncthreads();                             // LDS reused by the next date
+        }
+        if (tid == 0) {
+            __threadfence();
+            last = atomicAdd(&defer[1], 1) == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        if (cnt > 0 && P.fin_var) fused_finalize<NT>(P, hdr, snaps, T);
+        __syncthreads();
+        if (tid == 0) {
+            defer[0] = 0;                                // reset for the next solve
+            defer[1] = 0;
+        }
     }
-    if (!P.fin_var) return;
-    __syncthreads();
-    if (!last) return;
-    fused_finalize<NT>(P, hdr, snaps, (long long)gridDim.x);
 }
 
 // LDS bytes of one k_compact workgroup (cfg 2, n = 256, Student: 31,952 B)

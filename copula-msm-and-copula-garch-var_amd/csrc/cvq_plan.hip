@@ -158,6 +158,9 @@ struct cvq_plan {
     std::vector<double> hvc;     // every v*(r, j >= 1), sorted (the bisection cells' node counts)
     int* d_ccount = nullptr;     // [4][1 << ccount_depth] cell node counts (nullptr: counted on device)
     int ccount_depth = -1;
+    int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
+    long long capDefer = 0;
+    bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
     // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
     // ub() of the fixed levels and the bisection trees for the cached solve arguments
     std::vector<double> hvs;
@@ -738,12 +741,44 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     return CVQ_OK;
 }
 
+// COMPACT's fast node path needs, per date: MSM, pi_t = f0 (x) f1 bit for bit (the
+// kernel's own test; compute_forecast_combinations builds it so); GARCH / UKF, finite
+// marginal tables -- proven here when every sigma is finite and |x| / sigma <= 6, so
+// u = Phi(x / sigma) stays inside [1e-9, 1 - 1e-9] (Student: nu >= 1).  Host inputs only.
+bool fast_path_proven(const StaticDev& S, const std::vector<double>& hx, long long T, const double* a,
+                      const double* b) {
+    if (S.dim != 2 || hx.empty()) return false;
+    if (S.model == CVQ_MSM) {
+        const int q = S.q;
+        for (long long t = 0; t < T; ++t) {
+            const double* f = a + t * 2 * q;
+            const double* pit = b + t * S.Q;
+            for (int l = 0; l < S.Q; ++l)
+                if (!(pit[l] == f[l / q] * f[q + l % q])) return false;
+        }
+        return true;
+    }
+    if (S.copula == CVQ_STUDENT && !(S.nu >= 1.0)) return false;
+    double xmax = 0.0;
+    for (double x : hx) xmax = std::max(xmax, std::fabs(x));
+    for (long long e = 0; e < 2 * T; ++e)
+        if (!(std::isfinite(a[e]) && a[e] > 0.0 && xmax <= 6.0 * a[e])) return false;
+    return true;
+}
+
+const char* solve_error_text(int err) {
+    return (err & 4) ? "a date needs the generic node path (pi not rank 1 or a non-finite marginal table entry) "
+                       "but the plan's fast-path hint said none would (cvq_set_fast_hint)"
+         : (err & 2) ? "bisection needs more iterations than the snapshot budget (K)"
+                     : "a date did not converge within the bisection budget (K)";
+}
+
 }  // namespace
 namespace cvq {
 int compact_max_n();                                                                  // cvq_compact.hip
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
-                   double* snaps, Header* hdr);
+                   double* snaps, Header* hdr, int* defer, bool generic);
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
                   const double* bounds, double* out, double* snaps, Header* hdr, double* stamps,
@@ -792,10 +827,15 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         double* st = nullptr;
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         if (dbg_stamps) st = (double*)p->d_stamps;
+        if (p->capDefer < p->T + 2) {                      // zeroed once; the generic kernel resets it
+            if ((rc = dev_alloc(&p->d_defer, (size_t)p->T + 2))) return rc;
+            CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
+            p->capDefer = p->T + 2;
+        }
         const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
                             p->ccount_depth >= 0 ? p->d_ccount : nullptr, p->ccount_depth};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
-                              snaps, hdr);
+                              snaps, hdr, p->d_defer, !p->fast_hint);
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
         // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
@@ -1220,7 +1260,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
@@ -1277,6 +1317,12 @@ int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
     return CVQ_OK;
 }
 
+int32_t cvq_set_fast_hint(cvq_plan* p, int32_t on) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    p->fast_hint = on != 0;
+    return CVQ_OK;
+}
+
 int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, int32_t mem) {
     CVQ_REQUIRE(p != nullptr && a != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(T > 0, CVQ_ERR_INVALID, "T must be > 0");
@@ -1309,6 +1355,7 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
         p->in_a = p->d_a;
         p->in_pi = p->d_pi;
     }
+    p->fast_hint = mem != CVQ_MEM_DEVICE && fast_path_proven(S, p->hx, T, a, b);
     if (S.model != CVQ_MSM && realloc) {          // GARCH/UKF: pi_t = [1.0] (Q = 1), set once
         std::vector<double> ones((size_t)p->capT * S.Q, 1.0);
         CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice,
@@ -1414,9 +1461,7 @@ int32_t cvq_solve_status(cvq_plan* p, int32_t* iters_out) {
     CVQ_HIP_CHECK(hipMemcpyAsync(err, p->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, p->stream));
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     if (iters_out) *iters_out = err[1];
-    CVQ_REQUIRE(err[0] == 0, CVQ_ERR_NUMERIC,
-                (err[0] & 2) ? "bisection needs more iterations than the snapshot budget (K)"
-                             : "a date did not converge within the bisection budget (K)");
+    CVQ_REQUIRE(err[0] == 0, CVQ_ERR_NUMERIC, solve_error_text(err[0]));
     return CVQ_OK;
 }
 
@@ -1456,6 +1501,7 @@ int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t
         int err[4] = {0, 0, 0, 0};
         CVQ_HIP_CHECK(hipMemcpyAsync(err, p->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, p->stream));
         CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+        CVQ_REQUIRE(!(err[0] & 4), CVQ_ERR_NUMERIC, solve_error_text(err[0]));
         if (err[0]) { K += 4; continue; }          // a date needed more than K iterations: widen
         if (iters_out) *iters_out = err[1];
         if (mem != CVQ_MEM_DEVICE) {

@@ -126,6 +126,16 @@ int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
  * (no copy); the caller keeps a and b alive and unchanged until the next call. */
 int32_t cvq_set_dates(cvq_plan* plan, int64_t T, const double* a, const double* b, int32_t mem);
 
+/* COMPACT: the caller asserts that every date of the current cvq_set_dates batch takes
+ * the fast node path -- MSM: b[t] is the outer product of the per-asset rows of a[t]
+ * bit for bit (compute_forecast_combinations, msm_estimation.py:392-418, and
+ * cvq_msm_tables build it so); GARCH / UKF: every marginal table entry is finite.  The
+ * solve then skips its deferred-date (generic path) kernel.  A date that violates the
+ * assertion fails the solve with CVQ_ERR_NUMERIC.  cvq_set_dates with CVQ_MEM_HOST sets
+ * the hint itself when it can prove it; CVQ_MEM_DEVICE clears it.  No reference
+ * counterpart (a launch-count optimisation of the device-resident path). */
+int32_t cvq_set_fast_hint(cvq_plan* plan, int32_t on);
+
 /* Drop-in for ValueAtRiskCalcualtion.compute_integral (calc_var_class.py:179-212)
  * == calc_grids_and_integrals_results (calc_integral.py:8-119):
  * out[t] = integral of the joint copula density over the nested grid of

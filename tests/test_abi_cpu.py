@@ -76,6 +76,7 @@ def test_host_side_validation_without_gpu():
     assert lib.cvq_snap_stride(C.byref(a), C.byref(s)) == N.CVQ_OK
     assert 20 <= s.value <= 30
     assert lib.cvq_solve_status(None, C.byref(s)) == N.CVQ_ERR_INVALID
+    assert lib.cvq_set_fast_hint(None, 1) == N.CVQ_ERR_INVALID
 
 
 def test_in_sample_entry_points_validate_on_the_host():

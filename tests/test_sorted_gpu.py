@@ -123,7 +123,8 @@ def test_full_size_sweep_matches_sorted(cfg, T):
     assert np.array_equal(out["sorted"][0], out["sweep"][0])
 
 
-@pytest.mark.parametrize("case,strategy", [("cfg4_k4_n16", "sorted"), ("cfg2_n64", "sorted"), ("cfg2_n64", "sweep")])
+@pytest.mark.parametrize("case,strategy", [("cfg4_k4_n16", "sorted"), ("cfg2_n64", "sorted"), ("cfg2_n64", "sweep"),
+                                           ("cfg2_n64", "compact")])
 def test_generic_path_non_rank1_pi(case, strategy):
     """A pi that is not the product of per-asset forecasts forces the generic node
     path (full W contraction, create_grids.py:121-171); VaR must follow the oracle."""
@@ -247,3 +248,107 @@ def test_3d_general_layout_n_above_128(copula):
         p.close()
     assert it == ref_it
     assert np.array_equal(var, ref)
+
+
+def _perturbed_pi(z, every):
+    pi = z["forecasts"].copy()
+    rng = np.random.default_rng(11)
+    pi[::every] *= rng.uniform(0.9, 1.1, size=pi[::every].shape)
+    return pi
+
+
+def test_compact_deferral_reuse():
+    """COMPACT's fast kernel defers the dates that need the generic node path (pi not
+    rank 1) to a second kernel, which also finalizes.  One plan solves a mixed batch,
+    an all-fast batch and an all-generic batch in turn: every VaR follows the oracle,
+    so the deferral count and the tickets are reset between solves."""
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden("cfg2_n64")
+    fbs = z["forecasts_by_states"]
+    args = (str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+            z["combos"], z["weights"], z["copula_params"])
+    p = QuadraturePlan(*args, vol_states=z["unique_vol_states"], strategy="compact")
+    try:
+        for pi in (_perturbed_pi(z, 3), z["forecasts"], _perturbed_pi(z, 1), z["forecasts"]):
+            P = Problem(*args, (fbs, pi), z["unique_vol_states"])
+            ref, ref_it, _ = calc_var(P.compute_integral, P.T, float(z["ptf_mean"]))
+            p.set_dates((fbs, pi))
+            var, it = p.calc_var(float(z["ptf_mean"]))
+            assert it == ref_it
+            assert np.array_equal(var, ref)
+    finally:
+        p.close()
+
+
+def test_compact_deferral_sharded():
+    """The deferral in the sharded (unfused) solve: per-rank cvq_solve_local with some
+    generic dates in each block, then every rank finalizes the whole vector."""
+    import torch
+    from copula_var import engine
+    from copula_var.distributed import shard
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden("cfg2_n64")
+    fbs, pi = z["forecasts_by_states"], _perturbed_pi(z, 4)
+    cargs = (str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+             z["combos"], z["weights"], z["copula_params"])
+    P = Problem(*cargs, (fbs, pi), z["unique_vol_states"])
+    ref, _, _ = calc_var(P.compute_integral, P.T, float(z["ptf_mean"]))
+    T, ranks = P.T, 3
+    args = engine.solve_args(float(z["ptf_mean"]))
+    stride = engine.QuadraturePlan.snap_stride(args)
+    dev = torch.device("cuda", 0)
+    per = shard(T, 0, ranks)[2]
+    hdr_all = torch.zeros(2 * ranks, dtype=torch.int64, device=dev)
+    snaps_all = torch.full((ranks * per, stride), float("nan"), dtype=torch.float64, device=dev)
+    plans = []
+    try:
+        for r in range(ranks):
+            lo, hi, _ = shard(T, r, ranks)
+            p = QuadraturePlan(*cargs, vol_states=z["unique_vol_states"], strategy="compact")
+            plans.append(p)
+            p.set_stream(torch.cuda.current_stream().cuda_stream)
+            p.set_dates((fbs[lo:hi], pi[lo:hi]))
+            p.solve_local(args, hdr_all[2 * r: 2 * r + 2].data_ptr(), snaps_all[r * per: r * per + (hi - lo)].data_ptr())
+        var = torch.empty(T, dtype=torch.float64, device=dev)
+        plans[0].solve_finalize(args, hdr_all.data_ptr(), ranks, snaps_all.data_ptr(), per, T, var.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(var.cpu().numpy(), ref)
+    finally:
+        for p in plans:
+            p.close()
+
+
+def test_compact_fast_hint_violation_fails_loudly():
+    """set_dates_device(fast=True) skips the deferred-date kernel; a date whose pi is not
+    rank 1 then fails the solve (CVQ_ERR_NUMERIC) instead of returning a VaR.  The same
+    inputs without the hint solve to the oracle's VaR."""
+    import torch
+    from copula_var import engine
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden("cfg2_n64")
+    fbs, pi = z["forecasts_by_states"], _perturbed_pi(z, 5)
+    cargs = (str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+             z["combos"], z["weights"], z["copula_params"])
+    P = Problem(*cargs, (fbs, pi), z["unique_vol_states"])
+    ref, _, _ = calc_var(P.compute_integral, P.T, float(z["ptf_mean"]))
+    dev = torch.device("cuda", 0)
+    d_a = torch.tensor(np.ascontiguousarray(fbs), dtype=torch.float64, device=dev)
+    d_b = torch.tensor(np.ascontiguousarray(pi), dtype=torch.float64, device=dev)
+    args = engine.solve_args(float(z["ptf_mean"]))
+    p = QuadraturePlan(*cargs, vol_states=z["unique_vol_states"], strategy="compact")
+    try:
+        p.set_stream(torch.cuda.current_stream().cuda_stream)
+        var = torch.empty(P.T, dtype=torch.float64, device=dev)
+        p.set_dates_device(P.T, d_a.data_ptr(), d_b.data_ptr(), fast=True)
+        p.solve_device(args, var.data_ptr())
+        with pytest.raises(RuntimeError, match="generic node path"):
+            p.solve_status()
+        p.set_dates_device(P.T, d_a.data_ptr(), d_b.data_ptr())
+        p.solve_device(args, var.data_ptr())
+        p.solve_status()
+        assert np.array_equal(var.cpu().numpy(), ref)
+    finally:
+        p.close()
