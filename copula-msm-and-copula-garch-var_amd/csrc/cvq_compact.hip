@@ -36,12 +36,13 @@ constexpr long long kGenericGrid = 512;
 template <int COP, bool MSM, int PM, bool FUSED, int RPT>
 void launch_r(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
-    const size_t lds = compact_lds_bytes(L.S.n, NT, L.G.nb, kColgInRow<COP>);
-    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, false>), dim3((unsigned)L.T), dim3(NT), lds, L.stream,
+    const size_t lds_fast = compact_lds_bytes<COP, false>(L.S.n, NT, L.G.nb);
+    const size_t lds_gen = compact_lds_bytes<COP, true>(L.S.n, NT, L.G.nb);
+    hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, false>), dim3((unsigned)L.T), dim3(NT), lds_fast, L.stream,
                        L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.generic ? L.defer : nullptr, L.T);
     if (!L.generic) return;
     hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, true>), dim3((unsigned)std::min(L.T, kGenericGrid)),
-                       dim3(NT), lds, L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.defer, L.T);
+                       dim3(NT), lds_gen, L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.defer, L.T);
 }
 
 // rows per thread: ceil(n / NT) rounded up to 1, 2, 4 or 8 (n <= 8 NT)

@@ -51,7 +51,12 @@ namespace cvq {
 #endif
 constexpr int kTailPerLane = CVQ_TAIL_PER_LANE;     // tail nodes per lane of the tail wave
 constexpr int kTailCap = 64 * kTailPerLane;         // bracket size that switches to the tail
-constexpr int kRowRec = 8;                          // doubles per LDS row record
+// LDS row record (doubles): the generic kernel's [c0 c1 c2 c3 scale | z0 B0 wr]; the fast
+// kernel keeps only the fast constants, [c0 c1 scale -] (Plackett [c0 c1 c2 c3 scale -])
+template <int COP, bool GEN>
+constexpr int kRowRec = GEN ? 8 : (COP == CVQ_PLACKETT ? 6 : 4);
+template <int COP, bool GEN>
+constexpr int kScaleAt = (GEN || COP == CVQ_PLACKETT) ? 4 : 2;
 constexpr int kColRec = 2;                          // doubles per LDS column record (16 B: lanes at
                                                     // consecutive columns read conflict-free)
 constexpr int kCutFixed = 8;                        // int16 per row in the fixed-level cut table (HBM)
@@ -62,7 +67,7 @@ constexpr int kBucketsPerPoint = 4;                 // grid lookup buckets per g
 // Plackett slots [2], [3] for the Student / Gaussian kernels, and the LDS cut
 // table keeps 6 of the HBM table's 8 columns.
 template <int COP>
-constexpr bool kColgInRow = COP != CVQ_PLACKETT;
+constexpr bool kColgInRow = COP != CVQ_PLACKETT;      // (generic kernel only)
 #ifndef CVQ_COMPACT_WAVES
 #define CVQ_COMPACT_WAVES 0                         // min waves per SIMD (0: compiler default)
 #endif
@@ -199,19 +204,18 @@ struct FastRow {
     double c0, c1, c2, c3, scale;
 };
 
-template <int COP>
+template <int COP, int SI>
 __device__ __forceinline__ void fast_row_consts(const StaticDev& S, double z0, double B0, double wr, double* rec) {
     if constexpr (COP == CVQ_STUDENT) {
         rec[0] = fma(S.Ri[0] * S.inv_nu, z0 * z0, 1.0);                 // R_r  (k_direct's Rr)
         rec[1] = (S.Ri[1] + S.Ri[2]) * S.inv_nu * z0;                   // P_r
-        rec[2] = rec[3] = 0.0;
-        rec[4] = S.term1 * B0 * wr;
+        rec[SI] = S.term1 * B0 * wr;
     } else if constexpr (COP == CVQ_GAUSSIAN) {
         rec[0] = S.Ri[0] * (z0 * z0);
         rec[1] = (S.Ri[1] + S.Ri[2]) * z0;
-        rec[2] = rec[3] = 0.0;
-        rec[4] = S.term1 * B0 * wr;
+        rec[SI] = S.term1 * B0 * wr;
     } else {
+        static_assert(SI == 4, "Plackett row records hold four constants before the scale");
         const double th = S.theta, a1 = th - 1.0, u = z0;
         rec[0] = th * fma(a1, u, 1.0);                                   // num = c0 + c1 v
         rec[1] = th * a1 * fma(-2.0, u, 1.0);
@@ -221,7 +225,7 @@ __device__ __forceinline__ void fast_row_consts(const StaticDev& S, double z0, d
     }
 }
 
-template <int COP>
+template <int COP, int SI>
 __device__ __forceinline__ FastRow load_fast_row(const double* rec) {
     FastRow f;
     const double2 a = *(const double2*)rec;
@@ -234,7 +238,7 @@ __device__ __forceinline__ FastRow load_fast_row(const double* rec) {
     } else {
         f.c2 = f.c3 = 0.0;
     }
-    f.scale = rec[4];
+    f.scale = rec[SI];
     return f;
 }
 
@@ -396,10 +400,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
     double* col = lds;                              // [n][kColRec]: z_j, B'_j = B_j wc_j
     // [n][2]: B_j, wc_j (generic path), stride cgs; Student / Gaussian: row record slots [2], [3]
-    constexpr int cgs = kColgInRow<COP> ? kRowRec : 2;
-    double* rowr = col + kColRec * n + (kColgInRow<COP> ? 0 : 2 * n);   // [n][kRowRec]: c0 c1 c2 c3 scale | z0 B0 wr
-    double* colg = kColgInRow<COP> ? rowr + 2 : col + kColRec * n;
-    double* sx = rowr + kRowRec * n;                // [n] grid
+    // (generic kernel only; the fast kernel has no such words)
+    constexpr int RR = kRowRec<COP, GEN>, SI = kScaleAt<COP, GEN>;
+    constexpr bool cg_in_row = GEN && kColgInRow<COP>, cg_own = GEN && !kColgInRow<COP>;
+    constexpr int cgs = cg_in_row ? RR : 2;
+    double* rowr = col + kColRec * n + (cg_own ? 2 * n : 0);   // [n][RR] row records
+    double* colg = cg_in_row ? rowr + 2 : col + kColRec * n;
+    double* sx = rowr + RR * n;                     // [n] grid
     double2* tail = (double2*)(sx + n);             // [kTailCap] tail nodes: (v*, value)
     double* red = (double*)(tail + kTailCap);       // [2][3][NT / 64] reduction slots
     int* wtot = (int*)(red + 6 * (NT / 64));        // [NT / 64] scan slots (padded to 16 B)
@@ -481,13 +488,15 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (!isfinite(A[0]) || !isfinite(B[0]) || !isfinite(A[1]) || !isfinite(B[1])) bad |= 1;
         col[kColRec * i] = A[1];
         col[kColRec * i + 1] = B[1] * wc;
-        double* rr = rowr + kRowRec * i;
-        fast_row_consts<COP>(S, A[0], B[0], wr, rr);
-        colg[cgs * i] = B[1];                                      // after the row constants: may share rr[2..3]
-        colg[cgs * i + 1] = wc;
-        rr[5] = A[0];
-        rr[6] = B[0];
-        rr[7] = wr;
+        double* rr = rowr + RR * i;
+        fast_row_consts<COP, SI>(S, A[0], B[0], wr, rr);
+        if constexpr (GEN) {
+            colg[cgs * i] = B[1];                                  // may share rr[2..3] (Student / Gaussian)
+            colg[cgs * i + 1] = wc;
+            rr[5] = A[0];
+            rr[6] = B[0];
+            rr[7] = wr;
+        }
     }
     const double* pit = pi + t * S.Q;
     if constexpr (MSM) {                                          // rank-1 check of pi_t
@@ -530,12 +539,12 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             if (!fast) {
                 double acc = 0.0;
                 for (int j = j0; j <= j1; ++j)
-                    acc += generic_node<COP, MSM>(S, rowr + kRowRec * rr, col[kColRec * j], colg + cgs * j, rr, j,
+                    acc += generic_node<COP, MSM>(S, rowr + RR * rr, col[kColRec * j], colg + cgs * j, rr, j,
                                                   rank1, pit);
                 return acc;
             }
         }
-        const FastRow fr = load_fast_row<COP>(rowr + kRowRec * rr);
+        const FastRow fr = load_fast_row<COP, SI>(rowr + RR * rr);
         constexpr int IL = (COP == CVQ_STUDENT && PM == 0) ? 1 : kIlp;   // general pow: register bound
         double acc[IL];
 #pragma unroll
@@ -814,9 +823,12 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     }
 }
 
-// LDS bytes of one k_compact workgroup (cfg 2, n = 256, Student: 31,952 B)
-inline size_t compact_lds_bytes(int n, int nt, int nb, bool colg_in_row) {
-    return sizeof(double) * ((size_t)(kColRec + (colg_in_row ? 0 : 2) + kRowRec + 1) * n) + sizeof(double2) * kTailCap +
+// LDS bytes of one k_compact workgroup (cfg 2, n = 256, Student: fast 23,760 B -- six dates per CU --,
+// generic 31,952 B)
+template <int COP, bool GEN>
+inline size_t compact_lds_bytes(int n, int nt, int nb) {
+    constexpr int cg = (GEN && !kColgInRow<COP>) ? 2 : 0;
+    return sizeof(double) * ((size_t)(kColRec + cg + kRowRec<COP, GEN> + 1) * n) + sizeof(double2) * kTailCap +
            sizeof(double) * 6 * (nt / 64) + sizeof(int) * (((nt / 64) + 3) & ~3) +
            sizeof(int16_t) * ((size_t)kCutLds * n + nb);
 }
