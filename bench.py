@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--cpu-jobs", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=1,
                     help="1 GPU: also time end-to-end steps (device forecast tables + solve, from returns)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="independent batches in flight (one plan + HIP stream each); 1 = one batch at a time")
     ap.add_argument("--time-all", type=int, default=0,
                     help="HIP-event time every kernel kind (adds event records to the timed region)")
