@@ -29,12 +29,25 @@ def solve_args(ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_gue
                           float(min_var), float(max_var), float(lower), float(tolerance), float(ptf_mean))
 
 
-def auto_strategy(model: str, dim: int) -> str:
-    """The measured-fastest strategy per workload (cfg 1-5 on one MI355X):
-    COMPACT for 2-asset MSM (cfg 2: 17.5M vs SORTED 15.7M VaR-dates/s), SORTED for
-    2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for 3 assets (the only
-    strategy that runs the 128^3 grid of cfg 4)."""
-    return "compact" if (dim == 2 and model == "msm") else "sorted"
+SORTED_MAX_N = {2: 512, 3: 255}      # sorted_max_n (cvq_sorted_kernels.h)
+PREFIX_MAX_N_3D = 64                  # PREFIX solves at most 4096 rows (cvq_plan.hip pick_solve_shape)
+MATERIALISED = ("prefix", "sorted", "sweep")   # strategies that hold only nodes with level <= v_cap
+
+
+def auto_strategy(model: str, dim: int, n: Optional[int] = None) -> str:
+    """The measured-fastest strategy per workload (cfg 1-5 on one MI355X)
+    among those that run it: COMPACT for 2-asset MSM (cfg 2: 20.3M vs SORTED 16.4M
+    VaR-dates/s), SORTED for 2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for
+    3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
+    bounds the choice: 3-D SORTED takes n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
+    takes n > 255.  SORTED and PREFIX hold the nodes with level <= v_cap only;
+    QuadraturePlan(strategy="auto") routes a query above v_cap to an unrestricted
+    sibling plan (COMPACT / DIRECT in 2-D, SORTED with v_cap at the grid's top in 3-D)."""
+    if dim == 2:
+        return "compact" if model == "msm" else "sorted"
+    if n is None or n <= SORTED_MAX_N[3]:
+        return "sorted"
+    raise ValueError(f"3-asset grids support num_points <= {SORTED_MAX_N[3]} (SORTED), got {n}")
 
 
 class QuadraturePlan:
@@ -44,6 +57,8 @@ class QuadraturePlan:
                  copula_params, vol_states=None, v_cap: float = 0.0, device: int = 0,
                  strategy: str = "auto"):
         N.require_gpu()
+        self._ctor = (model, copula, dim, x_values, step, densities, combos, weights, copula_params, vol_states,
+                      device)
         self.model, self.copula, self.dim = model, copula, int(dim)
         self.device = int(device)
         self._x = N.f64(x_values)
@@ -68,13 +83,17 @@ class QuadraturePlan:
         st.vol_states = dp(self._vs) if self._vs is not None else None
         st.copula_params = dp(self._cp)
         st.n_copula_params = self._cp.size
+        self._auto = strategy == "auto"
+        self._wide: Optional["QuadraturePlan"] = None       # unrestricted sibling (auto, level > v_cap)
+        self._dates = None                                  # last set_dates / set_dates_device arguments
         if strategy == "auto":
-            strategy = auto_strategy(model, self.dim)
+            strategy = auto_strategy(model, self.dim, self._x.size)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
                        "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED,
                        "sweep": N.STRATEGY_SWEEP}[strategy]
         self.strategy = strategy
         st.v_cap = float(v_cap)
+        self.v_cap = float(v_cap)
         self._static = st
         h = C.c_void_p()
         N.check(N.lib().cvq_plan_create(C.byref(st), self.device, C.byref(h)), "cvq_plan_create")
@@ -86,9 +105,34 @@ class QuadraturePlan:
 
     # ------------------------------------------------------------ lifecycle
     def close(self) -> None:
+        if getattr(self, "_wide", None) is not None:
+            self._wide.close()
+            self._wide = None
         if getattr(self, "_h", None):
             N.lib().cvq_plan_destroy(self._h)
             self._h = None
+
+    # ------------------------------------------------------------ auto: levels above v_cap
+    def _route(self, top: float) -> "QuadraturePlan":
+        """The plan that serves a query reaching level `top`: this one, or (strategy
+        "auto" on a materialised strategy, top > v_cap) an unrestricted sibling --
+        COMPACT in 2-D (its slabs run k_direct, any bounds), SORTED in 3-D with v_cap
+        at the grid's top level -- holding the same per-date inputs."""
+        if not self._auto or self.strategy not in MATERIALISED or not (top > self.v_cap):
+            return self
+        if self._wide is None:
+            model, copula, dim, x, step, dens, combos, w, cp, vs, dev = self._ctor
+            if self.dim == 2:
+                self._wide = QuadraturePlan(model, copula, dim, x, step, dens, combos, w, cp, vol_states=vs,
+                                            device=dev, strategy="compact")
+            else:
+                grid_top = float(np.sum(np.abs(self._w)) * np.max(np.abs(self._x)))
+                self._wide = QuadraturePlan(model, copula, dim, x, step, dens, combos, w, cp, vol_states=vs,
+                                            v_cap=max(grid_top, float(top)), device=dev, strategy="sorted")
+            if self._dates is not None:
+                kind, args = self._dates
+                (self._wide.set_dates if kind == "host" else self._wide.set_dates_device)(*args)
+        return self._wide._route(top)
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -135,6 +179,10 @@ class QuadraturePlan:
             T = a.shape[0]
             N.check(N.lib().cvq_set_dates(self._h, T, N.ptr(a), None, N.MEM_HOST), "cvq_set_dates")
         self.T = int(T)
+        if self._auto:
+            self._dates = ("host", (integrations_params_t,))
+            if self._wide is not None:
+                self._wide.set_dates(integrations_params_t)
 
     def set_dates_device(self, T: int, a_ptr: int, b_ptr: Optional[int] = None, fast: bool = False) -> None:
         """Per-date inputs already resident in device memory (e.g. torch tensors' data_ptr()).
@@ -148,6 +196,10 @@ class QuadraturePlan:
         if fast:
             N.check(N.lib().cvq_set_fast_hint(self._h, 1), "cvq_set_fast_hint")
         self.T = int(T)
+        if self._auto:
+            self._dates = ("device", (T, a_ptr, b_ptr, fast))
+            if self._wide is not None:
+                self._wide.set_dates_device(T, a_ptr, b_ptr, fast)
 
     # ------------------------------------------------------------ quadrature
     def compute_integral(self, bounds) -> np.ndarray:
@@ -155,6 +207,10 @@ class QuadraturePlan:
         b = N.f64(bounds)
         if b.shape != (self.T, 2):
             raise ValueError(f"bounds must have shape ({self.T}, 2)")
+        top = float(np.nanmax(b)) if b.size else 0.0
+        target = self._route(top)
+        if target is not self:
+            return target.compute_integral(b)
         out = np.empty(self.T)
         N.check(N.lib().cvq_slab(self._h, N.ptr(b), N.ptr(out), N.MEM_HOST), "cvq_slab")
         return out
@@ -163,6 +219,11 @@ class QuadraturePlan:
                  **consts) -> Tuple[np.ndarray, int]:
         """Drop-in for calc_var (calc_var_class.py:95-177): returns (VaR (T,), iterations)."""
         args = solve_args(ptf_mean, obj_var, first_guess, second_guess, **consts)
+        top = max(args.first_guess, args.second_guess_lo, args.second_guess_hi, args.max_var, args.min_var,
+                  args.lower)
+        target = self._route(top)
+        if target is not self:
+            return target.calc_var(ptf_mean, obj_var, first_guess, second_guess, **consts)
         out = np.empty(self.T)
         it = C.c_int32(0)
         N.check(N.lib().cvq_solve(self._h, C.byref(args), N.ptr(out), C.byref(it), N.MEM_HOST), "cvq_solve")

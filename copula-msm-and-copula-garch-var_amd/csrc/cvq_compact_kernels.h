@@ -418,7 +418,12 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (stamps && tid == 0 && idx < 32) stamps[idx] = __builtin_amdgcn_s_memtime();
     };
     stamp(0);
-    if (stamps && tid == 0) stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+    if (stamps && tid == 0) {
+        stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+        // placement: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of this workgroup's first wave
+        stamps[27] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                     ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+    }
     int row[RPT];
     bool own[RPT];
 #pragma unroll

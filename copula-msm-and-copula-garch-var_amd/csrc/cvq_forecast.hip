@@ -81,8 +81,12 @@ struct Quad {
 
 // One Hamilton-filter step (calc_bayes_upd_numba, calc_prob.py:51-69) for a
 // quad-resident state vector.  v: this lane's SL states (state s = lane_q*SL + j),
-// cv: the matching conditional densities.  Returns the normaliser.
-template <int K>
+// cv: the matching conditional densities.  Returns the normaliser.  IEEE: normalise
+// by IEEE division, v / tot as calc_prob.py does (the reference-facing filter
+// cvq_msm_filter); else by a hardware reciprocal + two Newton steps (~1 ulp; the
+// blocked end-to-end filter and the likelihoods, where ~1e-16 is far below the 1e-8
+// node noise the VaR tolerates).
+template <int K, bool IEEE = false>
 __device__ __forceinline__ double msm_step(double (&v)[Quad<K>::SL], const double (&cv)[Quad<K>::SL],
                                            const MsmParams& P, bool* zero) {
     constexpr int SL = Quad<K>::SL, L = Quad<K>::L, LB = Quad<K>::LB;
@@ -115,8 +119,11 @@ __device__ __forceinline__ double msm_step(double (&v)[Quad<K>::SL], const doubl
     if (L >= 2) tot += quad_xor<1>(tot);
     if (L >= 4) tot += quad_xor<2>(tot);
     *zero = !(tot != 0.0);
-    // 1 / tot: hardware reciprocal + two Newton steps (~1 ulp; the reference's v / tot
-    // rounds differently by ~1e-16, far below the 1e-8 node noise the VaR tolerates)
+    if constexpr (IEEE) {
+#pragma unroll
+        for (int j = 0; j < SL; ++j) v[j] = v[j] / tot;
+        return tot;
+    }
     double inv = __builtin_amdgcn_rcp(tot);
     inv = fma(inv, fma(-tot, inv, 1.0), inv);
     inv = fma(inv, fma(-tot, inv, 1.0), inv);
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(256) void k_msm_filter(MsmParamsN PN, const double*
 #pragma unroll
                 for (int j = 0; j < SL; ++j) ring[d][j] = nx < n_in ? base[nx * S + j] : 0.0;
                 bool z;
-                msm_step<K>(v, cv, P, &z);
+                msm_step<K, true>(v, cv, P, &z);
                 bad |= z;
             }
         }

@@ -743,8 +743,11 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
 
 // COMPACT's fast node path needs, per date: MSM, pi_t = f0 (x) f1 bit for bit (the
 // kernel's own test; compute_forecast_combinations builds it so); GARCH / UKF, finite
-// marginal tables -- proven here when every sigma is finite and |x| / sigma <= 6, so
-// u = Phi(x / sigma) stays inside [1e-9, 1 - 1e-9] (Student: nu >= 1).  Host inputs only.
+// marginal tables -- proven here when every sigma is finite and |x| / sigma <= 6: then
+// u = Phi(x / sigma) lies in [Phi(-6), 1 - Phi(-6)] with Phi(-6) ~ 9.87e-10, i.e. strictly
+// inside (0, 1), so t.ppf / norm.ppf and the densities are finite (Student: nu >= 1, the
+// heaviest tail whose quantile at 9.87e-10 is still ~ -3.2e8; tests/test_fullsize_oracle_gpu.py
+// runs sigma = xmax / 6 exactly at nu = 1).  Host inputs only.
 bool fast_path_proven(const StaticDev& S, const std::vector<double>& hx, long long T, const double* a,
                       const double* b) {
     if (S.dim != 2 || hx.empty()) return false;

@@ -15,8 +15,15 @@ path (tests/golden/_shims), and writes inputs + the reference's outputs:
 * optim_msm_marg.npz -- calc_marginals / calc_densities
   (markov_switching_multifractal/calc_marginals.py:7-30, the in-sample MSM marginals
   and densities of msm_estimation.py:55-120) on the same returns and parameter rows.
+* optim_ukf.npz -- KalmanFilterVolEstimation(a, l, q, l, q, n, returns)
+  (kalman_mean_reverting/estimate.py:7-43 -> calculate_loglikelihood :230-281, called
+  so by forecast.py:9 and optimize.py:31): LL, filtered state path and the forecast
+  mean at a set of (a, l, q) rows on a synthetic OU-log-vol series.
+* optim_garch_pq.npz -- garch/forecast.py:5-19 calc_forecast(omega, alpha, beta,
+  window) for (p, q) in {(2,1), (1,2), (2,2), (3,2)} over rolling windows (the alpha /
+  beta lag order of Q13: alpha_1 pairs with the oldest of the last p returns).
 
-Usage:  python tests/golden/gen_optim_golden.py [all|msm_marginals]
+Usage:  python tests/golden/gen_optim_golden.py [all|msm_marginals|ukf_garch_pq]
 """
 from __future__ import annotations
 
@@ -116,9 +123,46 @@ def msm_marginals():
     print("msm marginals:", np.array(marg).shape, np.array(dens).shape)
 
 
+def ukf_garch_pq():
+    import matplotlib
+    matplotlib.use("Agg")
+    from kalman_mean_reverting.estimate import KalmanFilterVolEstimation
+    from garch.forecast import calc_forecast
+
+    cfg = synthetic.baseline_configs()[5].with_(T=1, n_in=1134)
+    r = synthetic.simulate_returns(cfg)[:, 0]
+    r = r - r.mean()
+    rows = [(0.97, 0.05, 0.15), (0.90, 0.0, 0.30), (0.99, -0.2, 0.10), (0.80, 0.30, 0.20), (0.5, 0.1, 0.5)]
+    ll, states, fc = [], [], []
+    for a, l, q in rows:
+        k = KalmanFilterVolEstimation(a, l, q, l, q, r.size, r)
+        ll.append(k.LL)
+        states.append(np.asarray(k.state_estimation, dtype=np.float64))
+        fc.append(k.forecasts)
+    np.savez(os.path.join(HERE, "optim_ukf.npz"), returns=r, rows=np.array(rows), ll=np.array(ll, dtype=np.float64),
+             states=np.array(states), forecast_mean=np.array(fc, dtype=np.float64))
+    print("ukf ll:", ll)
+
+    n_in, T = 400, 24
+    s = garch_series(n=n_in + T - 1, seed=11)
+    orders = [(2, 1), (1, 2), (2, 2), (3, 2)]
+    prm = {(2, 1): [0.05, 0.05, 0.03, 0.85], (1, 2): [0.04, 0.07, 0.5, 0.38],
+           (2, 2): [0.06, 0.04, 0.05, 0.45, 0.4], (3, 2): [0.05, 0.02, 0.03, 0.04, 0.5, 0.35]}
+    out = np.zeros((len(orders), T))
+    for i, (p, q) in enumerate(orders):
+        w = np.asarray(prm[(p, q)], dtype=np.float64)
+        for t in range(T):
+            out[i, t] = calc_forecast(w[0], w[1:p + 1], w[p + 1:], s[t:t + n_in])
+    np.savez(os.path.join(HERE, "optim_garch_pq.npz"), returns=s, n_in=n_in, orders=np.array(orders),
+             params=np.array([np.pad(prm[o], (0, 6 - len(prm[o]))) for o in orders]), forecasts=out)
+    print("garch pq forecasts:", out[:, :3])
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("all", "optim"):
         main()
     if what in ("all", "msm_marginals"):
         msm_marginals()
+    if what in ("all", "ukf_garch_pq"):
+        ukf_garch_pq()

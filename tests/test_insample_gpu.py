@@ -96,3 +96,31 @@ def test_pipeline_without_injected_parameters(case):
     cache = {"msm": A.SharedCacheCopulaMSMVaR, "garch": A.SharedCacheCopulaGarchVaR,
              "mean_reverting": A.SharedCacheCopulaMRVaR}[model].cache
     assert all((tk, kw["k"]) in cache if model == "msm" else tk in cache for tk in tickers)
+
+
+def test_ukf_kernels_match_reference_golden():
+    """cvq_ukf_filter / cvq_ukf_loglik / cvq_ukf_forecast against the reference's own
+    KalmanFilterVolEstimation(a, l, q, l, q, n, returns) (estimate.py:230-281; LL at :276,
+    forecast mean at :258/:281, Q19) at fixed (a, l, q) rows (golden optim_ukf)."""
+    from copula_var import engine
+    z = load_golden("optim_ukf")
+    r, P = z["returns"], z["rows"]
+    ll, st = engine.ukf_filter(r, P)
+    np.testing.assert_allclose(ll, z["ll"], rtol=1e-12)
+    np.testing.assert_allclose(st, z["states"], rtol=1e-11, atol=1e-13)
+    np.testing.assert_allclose(engine.ukf_loglik(r, P), z["ll"], rtol=1e-12)
+    for i, (a, l, q) in enumerate(P):
+        f = engine.ukf_forecast(r, r.size, a, l, q)          # one window = the whole series
+        np.testing.assert_allclose(np.log(f[0]), z["forecast_mean"][i], rtol=1e-12)
+
+
+def test_garch_forecast_pq_kernel_matches_reference_golden():
+    """cvq_garch_forecast_pq against garch/forecast.py:5-19 run by the reference for
+    (p, q) in {(2,1), (1,2), (2,2), (3,2)} (Q13 lag order), rolling windows."""
+    from copula_var import engine
+    z = load_golden("optim_garch_pq")
+    s, n_in = z["returns"], int(z["n_in"])
+    for i, (p, q) in enumerate(z["orders"]):
+        w = z["params"][i][:1 + p + q]
+        got = engine.garch_forecast_pq(s, n_in, int(p), int(q), w)
+        np.testing.assert_allclose(got, z["forecasts"][i], rtol=1e-13, err_msg=f"GARCH({p},{q})")

@@ -79,3 +79,32 @@ def test_msm_optimizer_host_logic_is_reproducible():
     assert 0.2 <= m0 <= 0.8 and 1.0 <= b <= 50.0 and 0.05 <= gamma <= 0.95
     np.testing.assert_allclose(sigma, np.sqrt(np.var(r)) / (m0 ** 2 - 2 * m0 + 2) ** (2 / 2), rtol=1e-15)
     assert runs[0][1] <= 6 + 2                                # <= one launch per iteration + start + final
+
+
+def test_oracle_ukf_filter_matches_reference():
+    """UKF E-step (kalman_mean_reverting/estimate.py:230-281, init (l, q) as forecast.py:9
+    and optimize.py:31 call it): LL, state path and forecast mean vs the reference's own
+    KalmanFilterVolEstimation (tests/golden/gen_optim_golden.py ukf_garch_pq)."""
+    from oracle.optim import ukf_filter_batch
+    from oracle.forecast import ukf_run
+    z = load_golden("optim_ukf")
+    ll, st = ukf_filter_batch(z["returns"], z["rows"])
+    np.testing.assert_allclose(ll, z["ll"], rtol=1e-12)
+    np.testing.assert_allclose(st, z["states"], rtol=1e-11, atol=1e-13)
+    for i, (a, l, q) in enumerate(z["rows"]):
+        f, _, _, failed = ukf_run(z["returns"][None, :], a, l, q)
+        assert not failed[0]
+        np.testing.assert_allclose(np.log(f[0]), z["forecast_mean"][i], rtol=1e-12)
+
+
+def test_oracle_optim_garch_pq_matches_reference():
+    """garch/forecast.py:5-19 for (p, q) != (1, 1): alpha_1 pairs with the oldest of the
+    last p returns (Q13), beta_1 with the oldest of the last q variances."""
+    from oracle.optim import garch_forecast_pq
+    z = load_golden("optim_garch_pq")
+    s, n_in = z["returns"], int(z["n_in"])
+    for i, (p, q) in enumerate(z["orders"]):
+        w = z["params"][i]
+        got = [garch_forecast_pq(s[t:t + n_in], w[0], w[1:p + 1], w[p + 1:p + 1 + q])
+               for t in range(z["forecasts"].shape[1])]
+        np.testing.assert_allclose(got, z["forecasts"][i], rtol=1e-14)

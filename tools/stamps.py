@@ -25,6 +25,23 @@ for _ in range(3):
 buf = np.zeros(T * 32, dtype=np.uint64)
 N.check(N.lib().cvq_plan_debug_stamps(p._h, N.ptr(buf), buf.size), "stamps")
 st = buf.reshape(T, 32).astype(np.int64)
+if STRAT == "compact" and (st[:, 27] != 0).any():
+    # placement: HW_ID bits cu 11:8, sh 12, se 15:13; XCC_ID low bits in the high word
+    hw = st[:, 27] & 0xFFFFFFFF
+    xcc = (st[:, 27] >> 32) & 0xF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 0x1
+    se = (hw >> 13) & 0x7
+    key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    uk, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    dur = (st[:, 26] - st[:, 25]).astype(np.float64)
+    print(f"placement: {uk.size} distinct CUs for {T} workgroups; per-CU count histogram "
+          f"{dict(zip(*np.unique(cnt, return_counts=True)))}; XCDs {np.unique(xcc).size}")
+    per_wg = cnt[inv]
+    for c in np.unique(per_wg):
+        m = per_wg == c
+        print(f"  WGs on a CU with {c} dates: {m.sum():5d}  duration mean {dur[m].mean():7.0f}  max {dur[m].max():7.0f}"
+              f" (10 ns ticks)")
 if STRAT == "direct":
     names = ["tables", "rowsetup", "slab1", "slab2", "bracket"] + [f"it{i}" for i in range(it)]
     cols = list(range(6 + it))
