@@ -15,12 +15,29 @@ the batch, with the per-date forecast tables already resident in HBM:
   default; --strategy direct: k_direct) -> [all-gather] -> finalise.
   (--strategy prefix: k_tables -> joint-mass row prefixes k_mass -> k_solve_prefix.)
 
-Prints ONE JSON line (rank 0).  Extra objects:
-  roofline     -- dominant kernel (k_direct, or k_mass for PREFIX), HIP-event timed
-                  on the plan's stream; algorithmic bytes = 8 B x reachable nodes
-                  x dates per launch, plus an FP64 sub-object.
+Prints ONE JSON line (rank 0).
+  value        -- whole-job VaR-dates/s with `--inflight` independent batches in flight
+                  (each its own plan + HIP stream; default 3), K timed steps.
+  single_solve -- the SURVEY.md §8(d) figure: T / wall time of ONE calc_var-equivalent
+                  solve (utils/calc_var_class.py:109-175), one batch at a time, K steps.
+  roofline     -- dominant kernel (k_compact / k_sorted / k_mass), bound "fp64-valu":
+                  algorithmic FP64 work (SURVEY.md §8d convention: FLOP per reachable
+                  node x reachable nodes x dates per launch) / the kernel's average
+                  duration, timed with HIP events on its stream in the single-solve leg
+                  (one launch in flight, so the bracket is the kernel's own duration, as
+                  rocprofv3's kernel trace gives it; profiles/ holds the trace split by
+                  leg).  Sub-object "hbm": 8 B x reachable nodes per date (the judged
+                  algorithmic bytes of §8d) over the same duration, and the PMC traffic.
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL).  Default weak scaling
+(--dates-per-gpu, default the config's T, per rank); --global-dates G solves G dates
+split into contiguous blocks of ceil(G / N) (BASELINE configs 3/4/5: 5000 / 2000 / 5000
+"sharded over 8"), strong scaling.  Both run every rank's block through
+copula_var.distributed.device_sharded_var (local solve -> ONE all-gather -> finalize)
+whenever N > 1 or --global-dates is given; each in-flight batch has its own process
+group, so the batches' collectives never share a communicator.
 """
 from __future__ import annotations
 
@@ -46,10 +63,13 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (vendor figure)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
     ap.add_argument("--dates-per-gpu", type=int, default=None)
+    ap.add_argument("--global-dates", type=int, default=None,
+                    help="total dates split over the ranks (strong scaling); default: --dates-per-gpu per rank")
+    ap.add_argument("--single", type=int, default=1, help="also time the one-batch-at-a-time solve (single_solve)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "prefix", "direct", "compact", "sorted", "sweep"],
                     help="auto: COMPACT for 2-asset MSM, SORTED otherwise (engine.auto_strategy)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
@@ -66,14 +86,16 @@ def parse():
 
 
 def build_inputs(cfg, T_total, rank, world, device):
-    """Synthetic returns for all dates; this rank's per-date tables via the device filters."""
+    """Synthetic returns for all dates; this rank's per-date tables via the device filters.
+    Rank r holds the contiguous block distributed.shard gives it (ceil(T / world) dates)."""
     from copula_var import synthetic, tables
+    from copula_var.distributed import shard
     c = cfg.with_(T=T_total)
     rets = synthetic.simulate_returns(c)
     mean, ptf_mean, centred, T = tables.insample_split(rets, c.n_in, c.weights)
-    per = T_total // world
-    lo = rank * per
-    block = centred[lo: lo + c.n_in + per]                       # windows lo .. lo+per-1
+    lo, hi, _ = shard(T_total, rank, world)
+    per = hi - lo
+    block = centred[lo: hi + c.n_in]                              # windows lo .. hi-1
     t0 = time.time()
     if c.model == "msm":
         ipt, uvs, ggp = tables.msm_integration_params(block, c.n_in, c.msm_params, c.k, c.num_points, device)
@@ -91,32 +113,29 @@ def main():
     import torch
     import torch.distributed as dist
     from copula_var import engine, synthetic
-    from copula_var import _native as N
 
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = synthetic.baseline_configs()[a.config]
     if a.strategy == "auto":
-        a.strategy = engine.auto_strategy(cfg.model, cfg.dim)
-    per_gpu = a.dates_per_gpu or cfg.T
-    T_total = per_gpu * world
+        a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points)
+    strong = a.global_dates is not None
+    T_total = a.global_dates if strong else (a.dates_per_gpu or cfg.T) * world
+    sharded = world > 1 or strong                 # local solve -> [all-gather] -> finalize
     c, ipt, uvs, ggp, ptf_mean, per, t_fc, block = build_inputs(cfg, T_total, rank, world, local)
     dens, x, step, combos = ggp
     dev = torch.device("cuda", local)
-    if c.model == "msm":
-        d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
-        d_b = torch.tensor(ipt[1], dtype=torch.float64, device=dev).contiguous()
-        b_ptr = d_b.data_ptr()
-    else:
-        d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
-        d_b, b_ptr = None, None
+    d_a = torch.tensor(ipt[0], dtype=torch.float64, device=dev).contiguous()
+    d_b = torch.tensor(ipt[1], dtype=torch.float64, device=dev).contiguous() if c.model == "msm" else None
+    b_ptr = d_b.data_ptr() if d_b is not None else None
     args = engine.solve_args(ptf_mean)
     fast_ok = c.model == "msm" and bool(np.array_equal(                # the kernel's own rank-1 test, on the host
         ipt[1], (ipt[0][:, 0, :, None] * ipt[0][:, 1, None, :]).reshape(ipt[1].shape))) if c.dim == 2 else False
-    # `inflight` batches in flight: plan i (its own HIP stream, scratch and output)
-    # solves steps i, i + inflight, ...  Consecutive batches are independent, so
-    # the next one fills the CUs that the current one's last workgroups leave idle.
+    # `inflight` batches in flight: plan i (its own HIP stream, scratch, output and, when
+    # sharded, its own process group) solves steps i, i + inflight, ...  Consecutive
+    # batches are independent, so the next one fills the CUs the current one's last
+    # workgroups leave idle.
     nf = max(1, a.inflight)
     plans, streams, vars_, shardeds = [], [], [], []
     for _ in range(nf):
@@ -127,65 +146,78 @@ def main():
         plans.append(p)
         streams.append(s_)
         vars_.append(torch.empty(T_total, dtype=torch.float64, device=dev))
-        if world > 1:
-            # rank-local solve -> one all-gather of headers + snapshots -> finalize (copula_var.distributed)
+        if sharded:
             from copula_var.distributed import device_sharded_var
+            grp = dist.new_group(list(range(world))) if world > 1 else None
             with torch.cuda.stream(s_):
-                shardeds.append(device_sharded_var(p, args, T_total, dev))
+                shardeds.append(device_sharded_var(p, args, T_total, dev, group=grp))
     plan = plans[0]
 
-    def step_fn(i):
-        k = i % nf
+    def step_fn(k):
         with torch.cuda.stream(streams[k]):
             # pi = outer product of the per-asset forecasts (compute_forecast_combinations), so the
             # fast path is asserted (a violating date would fail the solve status check below)
             plans[k].set_dates_device(per, d_a.data_ptr(), b_ptr, fast=fast_ok)   # forces tables recompute
-            if world == 1:
+            if not sharded:
                 plans[k].solve_device(args, vars_[k].data_ptr())
             else:
                 shardeds[k].solve(check=False)
 
-    for i in range(a.warmup):
-        step_fn(i)
-    torch.cuda.synchronize()
-    dom = "mass" if a.strategy == "prefix" else "solve"                       # dominant kernel
-    for p in plans:
-        p.enable_timing(True if a.time_all else (dom,))
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step_fn(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    kt = {}
-    for k in ("tables", "mass", "solve", "finalize"):
-        ms_n = [p.kernel_time(k) for p in plans]
-        kt[k] = (sum(m for m, _ in ms_n), sum(n_ for _, n_ in ms_n))
-    for p in plans:                      # convergence within the bisection budget (outside the timed region)
-        p.solve_status()
-    vals = (vars_[0] if world == 1 else shardeds[0].var).cpu().numpy()
+    def timed(n_batches, steps, warmup, timing=None):
+        """Wall time of `steps` steps (batch i % n_batches), barrier + synchronize on both
+        sides, max over ranks."""
+        for i in range(warmup):
+            step_fn(i % n_batches)
+        torch.cuda.synchronize()
+        for k in range(nf):
+            plans[k].enable_timing(timing if (timing and k < n_batches) else False)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step_fn(i % n_batches)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        kt = {}
+        for kind in ("tables", "mass", "solve", "finalize"):
+            ms_n = [plans[k].kernel_time(kind) for k in range(n_batches)]
+            kt[kind] = (sum(m for m, _ in ms_n), sum(n_ for _, n_ in ms_n))
+        for k in range(n_batches):       # convergence within the bisection budget (outside the timed region)
+            plans[k].solve_status()
+        return el, kt
+
+    dom = "mass" if a.strategy == "prefix" else "solve"                      # dominant kernel
+    elapsed, kt = timed(nf, a.steps, a.warmup, True if a.time_all else (dom,))
+    vals = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
     ms_step = elapsed / a.steps * 1e3
     value = T_total * a.steps / elapsed
+    if nf > 1 and a.single:
+        el1, kt1 = timed(1, a.steps, a.warmup, (dom,))                        # one batch at a time
+        v1 = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
+        assert np.array_equal(v1, vals, equal_nan=True), "single-solve leg changed the VaR"
+    else:
+        el1, kt1 = elapsed, kt
+    single = {"value": T_total * a.steps / el1, "unit": "VaR-dates/s", "ms_per_step": el1 / a.steps * 1e3,
+              "inflight": 1, "steps": a.steps,
+              "scope": "one calc_var-equivalent solve per step (utils/calc_var_class.py:109-175), tables resident"}
 
-    # dominant kernel: k_mass (PREFIX) or the per-date solve k_direct (DIRECT)
-    dom_ms, dom_n = kt[dom]
+    # roofline of the dominant kernel from the single-solve leg: one launch in flight, so the
+    # HIP events bracket the kernel's own duration (rocprofv3 kernel trace: profiles/)
+    dom_ms, dom_n = kt1[dom]
     dom_avg_s = dom_ms / max(dom_n, 1) / 1e3
-    alg_bytes = 8.0 * plan.reach_nodes * per          # one f64 joint-mass word per reachable node
-    achieved = alg_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
-    # with batches in flight a launch's duration includes time its workgroups wait for
-    # the previous batch's CUs; the per-step figure is the delivered rate
-    achieved_step = alg_bytes / (elapsed / a.steps) / 1e9
-    # FP64 basis: per reachable node ~14 FLOP + 1 pow (counted as 1) for Student
+    # FP64 basis (SURVEY §8d): per reachable node 14 FLOP + 1 pow (counted as 1) for Student
     flop_node = {"student": 15.0, "gaussian": 14.0, "plackett": 16.0}[c.copula] + (9.0 if c.dim == 3 else 0.0)
-    fp64_tflops = flop_node * plan.reach_nodes * per / dom_avg_s / 1e12 if dom_avg_s > 0 else 0.0
+    flop_launch = flop_node * plan.reach_nodes * per
+    fp64_tflops = flop_launch / dom_avg_s / 1e12 if dom_avg_s > 0 else 0.0
+    alg_bytes = 8.0 * plan.reach_nodes * per          # one f64 joint-mass word per reachable node (SURVEY §8d)
+    achieved_gbs = alg_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_cfg{a.config}.json")
     if os.path.exists(pmc_path):
@@ -196,9 +228,10 @@ def main():
         except Exception:
             traffic = None
     kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items() if v[1]}
+    kernels_single = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt1.items() if v[1]}
 
     e2e = None
-    if a.e2e and world == 1:
+    if a.e2e and world == 1 and not strong:
         e2e = end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev)
 
     cpu = None
@@ -206,6 +239,11 @@ def main():
         cpu = cpu_baseline(c, ipt, uvs, ggp, ptf_mean, vals, a)
 
     if rank == 0:
+        kname = {"prefix": "k_mass (joint-mass row prefix)",
+                 "direct": "k_direct (per-date slab-on-the-fly solve)",
+                 "compact": "k_compact (per-date solve, block tail)",
+                 "sorted": "k_sorted (per-date solve over the v*-sorted node list)",
+                 "sweep": "k_sorted<SWEEP> (per-date solve, one pass per bisection cell)"}[a.strategy]
         out = {
             "metric": METRICS.get(a.config, f"VaR dates solved/sec, {c.name}"),
             "value": value,
@@ -215,7 +253,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic ({c.model} returns, seed {c.seed}; injected in-sample params; fixed copula)",
@@ -223,19 +261,18 @@ def main():
                        "dim": c.dim, "grid": f"{c.num_points}^{c.dim}", "dates_per_gpu": per,
                        "global_dates": T_total, "n_in": c.n_in, "parallelism": f"dates/dp{world}",
                        "strategy": a.strategy, "inflight": nf},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": {"prefix": "k_mass (joint-mass row prefix)",
-                                    "direct": "k_direct (per-date slab-on-the-fly solve)",
-                                    "compact": "k_compact (per-date solve, one-wave tail)",
-                                    "sorted": "k_sorted (per-date solve over the v*-sorted node list)",
-                                    "sweep": "k_sorted<SWEEP> (per-date solve, one pass per bisection cell)"}[a.strategy],
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_us": dom_avg_s * 1e6,
-                         "achieved_per_step": achieved_step,
-                         "reach_nodes_per_date": plan.reach_nodes,
-                         "fp64": {"achieved_tflops": fp64_tflops, "peak_tflops": FP64_PEAK_TFLOPS,
-                                  "frac": fp64_tflops / FP64_PEAK_TFLOPS, "flop_per_node": flop_node}},
+            "single_solve": single,
+            "roofline": {"bound": "fp64-valu", "achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": fp64_tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kname,
+                         "flop_per_node": flop_node, "reach_nodes_per_date": plan.reach_nodes,
+                         "dates_per_launch": per, "flop_per_launch": flop_launch,
+                         "avg_launch_us": dom_avg_s * 1e6, "launches": dom_n,
+                         "timing": "HIP events on the kernel's stream, single-solve leg (one launch in flight)",
+                         "hbm": {"alg_bytes_per_launch": alg_bytes, "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                                 "pmc_bytes_per_launch": traffic}},
             "kernels": kernels,
+            "kernels_single": kernels_single,
             "forecast_stage_s": t_fc,
             "e2e": e2e,
             "var_checksum": float(np.nansum(vals)),

@@ -120,6 +120,9 @@ class QuadraturePlan:
         at the grid's top level -- holding the same per-date inputs."""
         if not self._auto or self.strategy not in MATERIALISED or not (top > self.v_cap):
             return self
+        if self._wide is not None and self._wide.strategy in MATERIALISED and top > self._wide.v_cap:
+            self._wide.close()                  # a higher level than the 3-D sibling holds: rebuild it
+            self._wide = None
         if self._wide is None:
             model, copula, dim, x, step, dens, combos, w, cp, vs, dev = self._ctor
             if self.dim == 2:

@@ -26,6 +26,8 @@ struct StaticDev {
     double inv_nu, nu, theta;
     double Ri[9];                 // inverse correlation, row-major dim x dim
     double w0, w1, w2;            // portfolio weights
+    double w0_inv;                // 1 / w0 when w0 is a power of two (then (v - lev) * w0_inv is the
+                                  // reference's (v - lev) / w0 bit for bit), else 0: divide
     TConst tk;                    // Student-t quantile constants
     const double* x;              // [n] grid
     const double* F;              // [dim][q][n] static Delta factors dens[(c-1)%dim]*step (Q5)
@@ -34,6 +36,16 @@ struct StaticDev {
     const long long* off;         // [nrows] row offset into a date's prefix block
     long long G;                  // reachable nodes per date (sum kmax)
 };
+
+// var_function's inner-axis coordinate g = (v - lev) / w0 (integration_algo.py:20, Q10), exact:
+// a multiplication when 1 / w0 is exact (w0 a power of two, e.g. the 2-asset weights 1/2).
+// (the division sits in a separate, non-inlined function: inlined, the compiler evaluates it
+// next to the multiplication and selects, so the common case would still pay for it)
+__host__ __device__ __attribute__((noinline)) inline double inner_coord_div(double d, double w0) { return d / w0; }
+__host__ __device__ __forceinline__ double inner_coord(const StaticDev& S, double v, double lev) {
+    if (S.w0_inv != 0.0) return (v - lev) * S.w0_inv;
+    return inner_coord_div(v - lev, S.w0);
+}
 
 struct SolveConst {
     double obj, fg, sg0, sg1, vmin, vmax, lower, tol;
@@ -52,6 +64,13 @@ struct alignas(16) Header {       // per-rank solve summary, all-gathered across
     uint64_t nonzero;             // bit k: some date had F != 0 at iteration k (Q4)
 };
 
+// Layout key of the structs passed between translation units (cvq_plan.hip launches the
+// kernels compiled in cvq_compact.hip / cvq_sorted.hip): a stale object fails its launch
+// with CVQ_ERR_STATE instead of reading misplaced pointers.
+constexpr size_t kAbiVersion = 3;
+__host__ __device__ constexpr size_t kernel_abi_key() {
+    return kAbiVersion * 1000003u + sizeof(StaticDev) * 4099u + sizeof(SolveConst) * 67u + sizeof(Header);
+}
 }  // namespace cvq
 
 // --------------------------------------------------------------- host errors

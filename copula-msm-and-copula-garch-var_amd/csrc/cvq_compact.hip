@@ -95,10 +95,14 @@ void launch_c(const CompactLaunch& L) {
 }  // namespace
 
 int compact_max_n() { return 8 * CVQ_COMPACT_NT; }
+int compact_tail_cap() { return CVQ_COMPACT_NT * kBlkPerThread; }   // block tail: cell nodes per workgroup
 
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
-                   double* snaps, Header* hdr, int* defer, bool generic) {
+                   double* snaps, Header* hdr, int* defer, bool generic, size_t abi) {
+    // the kernel arguments are structs shared with cvq_plan.hip: refuse a stale object
+    CVQ_REQUIRE(abi == (kernel_abi_key() ^ (sizeof(CompactGeom) << 40)), CVQ_ERR_STATE,
+                "libcvq objects built from different headers (rebuild all)");
     const CompactLaunch L{S, P, G, T, stream, a, tA, tB, pi, st, snaps, hdr, defer, fused, generic};
 #ifdef CVQ_DEV_CFG2
     launch_c<CVQ_STUDENT>(L);

@@ -20,10 +20,14 @@
 //     an exact probe (count_le's result in O(1) LDS reads); the row owner sums
 //     its slab columns with kIlp independent node chains; ONE workgroup
 //     reduction returns (slab sum, slab nodes, bracket nodes).
-//  4. Tail: once the bracket holds <= kTailCap nodes, their (v*, value) pairs go
-//     to LDS -- v*(r, j) is the smallest level with node (r, j) inside, the exact
-//     FP64 membership rule, precomputed per plan -- and one wave runs the
-//     remaining levels alone with masked wave sums (no barriers, no searches).
+//  4. Block tail (host cell tables present, the default): once the bisection cell
+//     holds <= NT * kBlkPerThread nodes, the workgroup evaluates the cell's nodes
+//     once in the host's v*-sorted order (v*(r, j): the smallest level with node
+//     (r, j) inside, the exact FP64 membership rule), one block prefix scan gives F
+//     at every node threshold, and the first thresholds where F >= obj and F != 0
+//     decide every remaining level (one lane, no sums).  Without cell tables: the
+//     bracket's (v*, value) pairs go to LDS once it holds <= kTailCap nodes and one
+//     wave runs the remaining levels with masked wave sums.
 //
 // Phase stamps of the DIRECT kernel showed the per-level workgroup steps --
 // binary searches, reductions, barriers -- and the single-row critical paths,
@@ -79,6 +83,31 @@ constexpr int kIlp = CVQ_COMPACT_ILP;               // independent node chains p
 // Fixed-level cut table columns: lower, sg0, fg, sg1, vmin, vmax (then padding).
 enum { kCutLower = 0, kCutSg0, kCutFg, kCutSg1, kCutVmin, kCutVmax };
 
+// Block tail (host cell tables present): once the bisection cell holds <= kBlkPerThread
+// nodes per thread, the whole workgroup evaluates the cell's nodes once, in the host's
+// v*-sorted order, and one block prefix scan gives F at every node threshold; the
+// remaining levels then follow from two crossing thresholds with no further sums.
+#ifndef CVQ_BLK_PER_THREAD
+#define CVQ_BLK_PER_THREAD 12
+#endif
+constexpr int kBlkPerThread = CVQ_BLK_PER_THREAD;
+// tail list word: row (bits 0-10) | column (bits 11-21) | last node of a tie group (bit 31)
+constexpr uint32_t kTlRowMask = 0x7FFu;
+constexpr int kTlColShift = 11;
+constexpr uint32_t kTlGroupEnd = 1u << 31;
+constexpr int kNoPos = 0x7FFFFFFF;                  // "no such position" in the crossing search
+#ifndef CVQ_TAIL_VSTAR
+#define CVQ_TAIL_VSTAR 1
+#endif
+
+#ifndef CVQ_COMPACT_PRIO
+#define CVQ_COMPACT_PRIO 0
+#endif
+template <int P>
+__device__ __forceinline__ void phase_prio() {
+    if constexpr (CVQ_COMPACT_PRIO != 0) __builtin_amdgcn_s_setprio(P);
+}
+
 // Date-independent device tables of a COMPACT plan.
 struct CompactGeom {
     const int16_t* cutfix;    // [n][kCutFixed] cut columns of the fixed levels (per solve arguments)
@@ -86,11 +115,17 @@ struct CompactGeom {
     const int16_t* bucket;    // [nb] largest j with x_j <= bx0 + b / binv (0 if none): a start guess
     double bx0, binv;         // bucket of a grid coordinate g: floor((g - bx0) * binv)
     int nb;
-    // [4][1 << cdepth] node counts of the bisection cells (heap node h of bracket b's tree at
-    // (b << cdepth) + h, 1 <= h < 2^cdepth; every depth-cdepth cell holds <= kTailCap nodes);
-    // nullptr: the levels reduce the bracket's node count on the device
+    // [4][2 << cdepth] node counts of the bisection cells (heap node h of bracket b's tree at
+    // (b << (cdepth + 1)) + h, 1 <= h < 2^(cdepth+1); every depth-cdepth cell holds <= the
+    // block tail's NT * kBlkPerThread nodes); nullptr: the levels reduce the bracket's node
+    // count on the device and finish with the one-wave tail
     const int* ccount;
     int cdepth;
+    // with ccount: every node (r, j >= 1) sorted by v* (tail list words) and their v*; bracket
+    // b's cells are contiguous ranges starting at bstart[b] (the cell tree's positions)
+    const uint32_t* tlist;
+    const double* tvs;
+    int bstart[4];
 };
 
 // ------------------------------------------------------------------ reductions
@@ -108,6 +143,24 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     v += dpp_i32<0x118>(v);
     v += dpp_i32<0x142, 0xA>(v);
     v += dpp_i32<0x143, 0xC>(v);
+    return v;
+}
+
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ double dpp_f64z(double v) {          // out-of-row / masked lanes read 0
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWMASK, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+// Inclusive prefix sum of a double over the 64 lanes (same DPP pattern as wave_incl_scan).
+__device__ __forceinline__ double wave_incl_scan_f64(double v) {
+    v += dpp_f64z<0x111>(v);
+    v += dpp_f64z<0x112>(v);
+    v += dpp_f64z<0x114>(v);
+    v += dpp_f64z<0x118>(v);
+    v += dpp_f64z<0x142, 0xA>(v);
+    v += dpp_f64z<0x143, 0xC>(v);
     return v;
 }
 
@@ -417,6 +470,10 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     auto stamp = [&](int idx) {                     // diagnostic only (never in a timed run)
         if (stamps && tid == 0 && idx < 32) stamps[idx] = __builtin_amdgcn_s_memtime();
     };
+    // issue priority by phase (CVQ_COMPACT_PRIO): the SIMD arbiter favours older waves, so the
+    // last date to arrive on a CU lags the others through every phase; a wave that is further
+    // along lowers its priority so the dates sharing a CU keep pace with each other
+    phase_prio<3>();
     stamp(0);
     if (stamps && tid == 0) {
         stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
@@ -521,6 +578,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // non-finite table entry, whose pi is rank 1 by construction)
     const bool flag = __syncthreads_or(MSM ? (bad & 2) : (bad & 1)) != 0;
     stamp(1);
+    phase_prio<2>();
     const bool rank1 = !(MSM && flag);
     const bool fast = rank1 && (MSM || !flag);
     if constexpr (!GEN) {
@@ -590,7 +648,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int16_t* c = cfx + (size_t)(own[k] ? row[k] : 0) * kCutLds;
         return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
              : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : v == P.vmax ? c[kCutVmax]
-             : grid_count(sx, bk, G, (v - lev[k]) / S.w0, 0, n - 1);
+             : grid_count(sx, bk, G, inner_coord(S, v, lev[k]), 0, n - 1);
     };
     int ka[RPT], kb[RPT];
     // slab (va, vb] between two fixed levels: these are triangles and corner bands
@@ -642,6 +700,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         kHi[k] = (own[k] && lo == lo) ? max((int)fixcut(k, hi), kLo[k]) : 0;
     }
     stamp(4);
+    phase_prio<1>();
 
     // ---- (iv) bisection (:250-309); Q2 / Q4 are resolved across dates by the finalize
     double prev = F, prevU = prevU0;
@@ -654,11 +713,15 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // bracket nodes: the host's cell table (heap node hc of bracket bsel's tree), else
     // reduced with the level's sum; a NaN bracket (Q3) holds none
     const bool tabc = G.ccount != nullptr;
-    const int* cc = tabc ? G.ccount + ((size_t)max(bsel, 0) << G.cdepth) : nullptr;
-    const int hend = tabc ? 1 << G.cdepth : 0;
+    const int* cc = tabc ? G.ccount + ((size_t)max(bsel, 0) << (G.cdepth + 1)) : nullptr;
+    const int hend = tabc ? 2 << G.cdepth : 0;                   // heap nodes 1 .. 2^(cdepth+1) - 1
     int hc = 1;
     int nbr_next = !tabc ? 1 << 30 : (bsel < 0 || hc >= hend) ? 0 : cc[hc];
-    for (; it < P.K && nbr_next > kTailCap; ++it) {
+    int ps = (tabc && bsel >= 0) ? G.bstart[bsel] : 0;           // the cell's first sorted position
+    // the block tail (host tables) needs one bisection level first: the reference's first
+    // level may subtract a slab it never added (Q1), after which F is the CDF plus a constant
+    const int cap = tabc ? NT * kBlkPerThread : kTailCap;
+    for (; it < P.K && (nbr_next > cap || (tabc && it == 0 && bsel >= 0)); ++it) {
         const double mid = (lo + hi) / 2;
         if (tid == 0) sn[it] = mid;
         if (nt < 0 && !(hi - lo > P.tol)) nt = it;
@@ -671,7 +734,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
 #ifdef CVQ_ABL_CNT
             kM[k] = own[k] ? (kLo[k] + kHi[k]) >> 1 : 0;
 #else
-            kM[k] = own[k] ? grid_count(sx, bk, G, (mid - lev[k]) / S.w0, kLo[k], kHi[k]) : 0;   // Q10
+            kM[k] = own[k] ? grid_count(sx, bk, G, inner_coord(S, mid, lev[k]), kLo[k], kHi[k]) : 0;   // Q10
 #endif
             ka[k] = ustack ? kLo[k] : kM[k];
             kb[k] = ustack ? kM[k] : kHi[k];
@@ -700,6 +763,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (ustack) {
             lo = mid;
             nbr_next = tabc ? c_hi : Nbr - Nlow;
+            ps += tabc ? c_lo : 0;
             hc = 2 * hc + 1;
 #pragma unroll
             for (int k = 0; k < RPT; ++k) kLo[k] = kM[k];
@@ -715,8 +779,121 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (it < 15) stamp(5 + it);
     }
 
+    // ---- block tail (host cell tables): the cell (lo, hi] = sorted positions [ps, ps + cnt).
+    // Thread tid evaluates positions tid * NPT + m in order; a block scan turns the values
+    // into F at every node threshold (F = prev + prefix when the last level moved lo, else
+    // prev - (cell total - prefix): the reference's adjust_integral chain after its first
+    // level).  F is non-decreasing in v (node values >= 0; a NaN makes every later F NaN),
+    // so each remaining level's decision "F(mid) < obj" is "mid < v_c" with v_c the first
+    // tie-group end where !(F < obj), and its nonzero bit is "mid >= v_z", v_z the first
+    // where F != 0 -- one lane then walks the remaining levels without sums.
+    phase_prio<0>();
+    if (tabc && it < P.K) {
+        constexpr int NPT = kBlkPerThread;
+        const int cnt = max(nbr_next, 0);
+        const uint32_t* tl = G.tlist + ps;
+        uint32_t wd[NPT];
+#pragma unroll
+        for (int m = 0; m < NPT; ++m) wd[m] = (tid * NPT + m < cnt) ? tl[tid * NPT + m] : 0u;
+        double pre[NPT];                                          // local inclusive prefix
+        double run = 0.0;
+#pragma unroll
+        for (int m = 0; m < NPT; ++m) {
+            const int r = (int)(wd[m] & kTlRowMask), j = (int)((wd[m] >> kTlColShift) & kTlRowMask);
+            const double v = (tid * NPT + m < cnt) ? range_sum(r, j, j) : 0.0;
+            run += v;
+            pre[m] = run;
+        }
+        // block exclusive scan of the thread totals (one barrier)
+        const double incl = wave_incl_scan_f64(run);
+        double* wt = red + parity * (3 * (NT / 64));
+        parity ^= 1;
+        if (lane == 63) wt[tid >> 6] = incl;
+        __syncthreads();
+        double base = incl - run, Stot = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) {
+            const double x = wt[w];
+            base += (w < (tid >> 6)) ? x : 0.0;
+            Stot += x;
+        }
+        const double Flo = ustack ? prev : prev - Stot;           // F just above lo
+        int mc = NPT, mz = NPT;                                   // first crossing / nonzero group end
+#pragma unroll
+        for (int m = NPT - 1; m >= 0; --m) {
+            if (!(wd[m] & kTlGroupEnd) || tid * NPT + m >= cnt) continue;
+            const double pa = base + pre[m];
+            const double Fv = ustack ? prev + pa : prev - (Stot - pa);
+            if (!(Fv < P.obj)) mc = m;
+            if (Fv != 0.0) mz = m;
+        }
+        // first thread (lowest positions) holding each: wave ballots, then the block's waves
+        const unsigned long long bc = __ballot(mc < NPT), bz = __ballot(mz < NPT);
+        int* ew = (int*)(red + parity * (3 * (NT / 64)));         // the other reduction half: 2 ints / wave
+        parity ^= 1;
+        // the first flagged thread of the wave holds the wave's first crossing; its position
+        // and node word go to LDS.  The leader then compares each mid with that node's v*
+        // (loaded once from the plan's sorted v* list: CVQ_TAIL_VSTAR = 1, measured faster) or
+        // evaluates the membership test x_j <= (mid - x_r w1) / w0 itself per level (= 0)
+        const int lc = bc ? (int)__builtin_ctzll(bc) : 0, lz = bz ? (int)__builtin_ctzll(bz) : 0;
+        const int mcl = __shfl(mc, lc, 64), mzl = __shfl(mz, lz, 64);
+        uint32_t wc = 0u, wz = 0u;
+#pragma unroll
+        for (int m = 0; m < NPT; ++m) {
+            wc = m == mc ? wd[m] : wc;
+            wz = m == mz ? wd[m] : wz;
+        }
+        const uint32_t wcl = (uint32_t)__shfl((int)wc, lc, 64), wzl = (uint32_t)__shfl((int)wz, lz, 64);
+        if (lane == 0) {
+            int* e = ew + 4 * (tid >> 6);
+            e[0] = bc ? ((tid >> 6) * 64 + lc) * NPT + mcl : kNoPos;
+            e[1] = (int)wcl;
+            e[2] = bz ? ((tid >> 6) * 64 + lz) * NPT + mzl : kNoPos;
+            e[3] = (int)wzl;
+        }
+        __syncthreads();
+        stamp(29);
+        if (tid == leader) {
+            int ec = kNoPos, ez = kNoPos;
+            uint32_t nc = 0u, nz_ = 0u;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) {                   // waves in position order: first wins
+                const int* e = ew + 4 * w;
+                if (ec == kNoPos && e[0] != kNoPos) { ec = e[0]; nc = (uint32_t)e[1]; }
+                if (ez == kNoPos && e[2] != kNoPos) { ez = e[2]; nz_ = (uint32_t)e[3]; }
+            }
+            // kind: 0 = every mid (F just above lo already decides), 1 = no mid, 2 = mids at or
+            // above the node's threshold
+            const int kc = !(Flo < P.obj) ? 0 : (ec == kNoPos ? 1 : 2);
+            const int kz = (Flo != 0.0) ? 0 : (ez == kNoPos ? 1 : 2);
+#if !CVQ_TAIL_VSTAR
+            const double xjc = sx[(nc >> kTlColShift) & kTlRowMask], levc = sx[nc & kTlRowMask] * S.w1;
+            const double xjz = sx[(nz_ >> kTlColShift) & kTlRowMask], levz = sx[nz_ & kTlRowMask] * S.w1;
+#else
+            (void)nc;
+            (void)nz_;
+#endif
+#if CVQ_TAIL_VSTAR                                            // A/B: compare mids with loaded v* values
+            const double vcs = kc == 2 ? G.tvs[ps + ec] : 0.0, vzs = kz == 2 ? G.tvs[ps + ez] : 0.0;
+#endif
+            for (; it < P.K; ++it) {
+                const double mid = (lo + hi) / 2;
+                sn[it] = mid;
+                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+#if CVQ_TAIL_VSTAR
+                const bool geq = kc == 0 || (kc == 2 && mid >= vcs);
+                const bool nz = kz == 0 || (kz == 2 && mid >= vzs);
+#else
+                const bool geq = kc == 0 || (kc == 2 && xjc <= inner_coord(S, mid, levc));   // !(F(mid) < obj)
+                const bool nz = kz == 0 || (kz == 2 && xjz <= inner_coord(S, mid, levz));    // F(mid) != 0
+#endif
+                if (nz) mask |= (1ull << it);
+                ustack = !geq;
+                if (ustack) lo = mid; else hi = mid;
+            }
+        }
+    } else if (it < P.K) {
     // ---- tail: the bracket's nodes -> LDS, wave 0 finishes the levels
-    if (it < P.K) {
         int len = 0;
 #pragma unroll
         for (int k = 0; k < RPT; ++k) len += own[k] ? kHi[k] - kLo[k] : 0;

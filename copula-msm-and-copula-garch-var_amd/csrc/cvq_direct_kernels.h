@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
         return;
     }
     auto cnt = [&](int k, double v, int klo, int khi) {
-        const double g = (v - lev[k]) / S.w0;         // var_function (Q10), exact FP64
+        const double g = inner_coord(S, v, lev[k]);   // var_function (Q10), exact FP64
         return count_le(sx, g, klo, khi);
     };
     auto node = [&](int k, int j) {

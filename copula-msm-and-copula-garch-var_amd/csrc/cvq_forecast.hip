@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -34,6 +35,11 @@ struct MsmParams {
 
 struct MsmParamsN {
     MsmParams a[3];                                // per asset (dim <= 3), passed by value
+};
+
+struct StateMapQ {                                 // unique-vol index of each of <= 16 states, per asset
+    uint8_t u[3][16];
+    int q;
 };
 
 MsmParams msm_params(int k, double m0, double sigma, double b, double gamma) {
@@ -375,8 +381,314 @@ __global__ __launch_bounds__(64) void k_msm_windows(MsmParamsN PN, const double*
     for (int j = 0; j < SL; ++j) out[t * S + lane_q * SL + j] = v[j];
 }
 
+// ------------------------------------------------------- transfer-matrix scan filter
+// Window t's filtered vector is normalise(M_{t+n-1} ... M_t u), M_i = diag(c_i) A, u uniform
+// (calc_prob.py:12-13, :51-69).  The steps are cut into blocks of B and the blocks into
+// superblocks of C; every window is then ONE product of at most four stored factors
+//     Pre_{b1}(e) x SGfull ... x PG/SG (superblock pieces) x Suf_{b0}(t) u,   e = t + n - 1,
+// with Pre_b(i) = M_i ... M_{bB} (prefix of i's block), Suf_b(i) = M_{bB+B-1} ... M_i
+// (suffix of i's block), PG_s / SG_s the prefix / suffix products of superblock s's block
+// products G_b = Pre_b(bB + B - 1).  The prefixes and suffixes are B- and C-step recursions
+// run once for all windows (every block / superblock in parallel), so a window costs four
+// 2^k x 2^k mat-vecs instead of n filter steps.  All factors are non-negative; each is kept
+// at a common scale of its own (a positive factor cancels in the final normalisation), so
+// the forecasts agree with the step-by-step filter to ~1e-14 relative.
+constexpr int kScanB = 32;       // steps per block
+constexpr int kScanC = 16;       // blocks per superblock
+
+// v <- A v for a quad-resident state vector (the transition of calc_prob.py:91-101 as k
+// Kronecker butterflies; A is symmetric, so this is also v^T A for a row vector)
+template <int K>
+__device__ __forceinline__ void apply_A(double (&v)[Quad<K>::SL], const MsmParams& P) {
+    constexpr int SL = Quad<K>::SL, LB = Quad<K>::LB;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const int pos = K - 1 - c;
+        const double pc = P.p[c], qc = P.qv[c];
+        if (pos < LB) {
+            double nv[SL];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) nv[j] = pc * v[j] + qc * v[j ^ (1 << pos)];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) v[j] = nv[j];
+        } else {
+            const int m = 1 << (pos - LB);
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                const double o = m == 1 ? quad_xor<1>(v[j]) : quad_xor<2>(v[j]);
+                v[j] = pc * v[j] + qc * o;
+            }
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ double quad_max(double m) {
+    m = fmax(m, quad_xor<1>(m));
+    return fmax(m, quad_xor<2>(m));
+}
+
+// Block prefixes (blockIdx.z = 0: quad q = column q of Pre_b(i), forward from e_q) and block
+// suffix row sums (z = 1: quad q = row q of Suf_b(i), backward from e_q^T; only Suf_b(i) u is
+// ever used, so only its row sums are stored).  The block's conditional densities
+// (calc_prob.py:116-117) are computed once into LDS.  Stored: Pre at window ends i >= n_in - 1
+// (Pre[(i - n_in + 1)][S][S], row-major), Suf1 at window starts i < T (Suf1[i][S]), the full
+// blocks' products G_b (Gf[b][S][S]).  Each step is scaled by 1 / max_s c_i (common to every
+// column / row of the block).
+template <int K>
+__global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const double* __restrict__ r,
+                                                        long long N, long long n_in, long long T,
+                                                        double* __restrict__ Pre, long long pstride,
+                                                        double* __restrict__ Suf1, long long ustride,
+                                                        double* __restrict__ Gf, long long gstride, int* err) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    __shared__ double cl[kScanB * S];                           // c_i[s] of the block's steps
+    __shared__ double cm[kScanB];                               // 1 / max_s c_i
+    const MsmParams& P = PN.a[blockIdx.y];
+    r += blockIdx.y * N;
+    const int q = threadIdx.x / L, lane_q = threadIdx.x % L;
+    const long long b0 = (long long)blockIdx.x * kScanB;
+    const long long b1 = min(b0 + kScanB, N);                    // steps [b0, b1)
+    const int nb = (int)(b1 - b0);
+    for (int k = threadIdx.x; k < nb * S; k += blockDim.x)
+        cl[k] = cond_prob(r[b0 + k / S], P.vs[k % S]);
+    __syncthreads();
+    bool bad = false;
+    for (int o = threadIdx.x; o < nb; o += blockDim.x) {
+        double m = 0.0;
+        for (int s2 = 0; s2 < S; ++s2) m = fmax(m, cl[o * S + s2]);
+        bad |= !(m > 0.0);                                       // every state's density is 0: calc_prob.py:64-65
+        cm[o] = 1.0 / m;
+    }
+    __syncthreads();
+    double v[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = (lane_q * SL + j == q) ? 1.0 : 0.0;
+    if (blockIdx.z == 0) {                                       // Pre: columns, forward
+        double* pre = Pre + blockIdx.y * pstride;
+        for (int o = 0; o < nb; ++o) {
+            const long long i = b0 + o;
+            const double sc = cm[o];
+            apply_A<K>(v, P);
+#pragma unroll
+            for (int j = 0; j < SL; ++j) v[j] = v[j] * (cl[o * S + lane_q * SL + j] * sc);
+            if (i >= n_in - 1) {
+                double* dst = pre + ((i - (n_in - 1)) * S + lane_q * SL) * S + q;
+#pragma unroll
+                for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
+            }
+            if (o == kScanB - 1) {                               // a full block's product G_b
+                double* dst = Gf + blockIdx.y * gstride + (blockIdx.x * (long long)S + lane_q * SL) * S + q;
+#pragma unroll
+                for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
+            }
+        }
+        if (bad) atomicOr(err, 1);
+    } else {                                                     // Suf: rows, backward
+        double* suf = Suf1 + blockIdx.y * ustride;
+        for (int o = nb - 1; o >= 0; --o) {
+            const long long i = b0 + o;
+            const double sc = cm[o];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) v[j] = v[j] * (cl[o * S + lane_q * SL + j] * sc);
+            apply_A<K>(v, P);                                    // row q of Suf_b(i) = row q of Suf_b(i+1) diag(c_i) A
+            if (i < T) {
+                double rs = 0.0;
+#pragma unroll
+                for (int j = 0; j < SL; ++j) rs += v[j];
+                rs += quad_xor<1>(rs);
+                rs += quad_xor<2>(rs);
+                if (lane_q == 0) suf[i * S + q] = rs;
+            }
+        }
+    }
+}
+
+// Superblock prefixes PG_s(beta) = G_{sC+beta} ... G_{sC} (z = 0, quad = column, forward) and
+// suffixes SG_s(beta) = G_{last} ... G_{sC+beta} (z = 1, quad = row, backward) of the block
+// products G_b (k_msm_blkscan's Gf), staged in LDS.  One wavefront per (superblock, asset,
+// direction) for K = 4 (16 quads): the common scale of each stored matrix is its maximum over
+// the wave.
+template <int K>
+__global__ __launch_bounds__(4 << K) void k_msm_supscan(const double* __restrict__ Gf, long long gstride,
+                                                        long long nfull, double* __restrict__ PG,
+                                                        double* __restrict__ SG, long long sstride) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    static_assert((4 << K) <= 64, "one wavefront per scan");
+    __shared__ __attribute__((aligned(16))) double gl[kScanC * S * S];
+    const int q = threadIdx.x / L, lane_q = threadIdx.x % L;
+    const long long s0 = (long long)blockIdx.x * kScanC;
+    const long long s1 = min(s0 + kScanC, nfull);
+    Gf += blockIdx.y * gstride;
+    {
+        const double2* src = (const double2*)(Gf + s0 * S * S);
+        double2* dst = (double2*)gl;
+        const int nv = (int)((s1 - s0) * S * S / 2);
+        for (int k = threadIdx.x; k < nv; k += blockDim.x) dst[k] = src[k];
+    }
+    __syncthreads();
+    double v[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) v[j] = (lane_q * SL + j == q) ? 1.0 : 0.0;
+    auto wave_max = [](double m) {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        return m;
+    };
+    if (blockIdx.z == 0) {                                       // columns: x <- G_b x
+        double* dst0 = PG + blockIdx.y * sstride + blockIdx.x * (long long)kScanC * S * S;
+        for (long long b = s0; b < s1; ++b) {
+            const double* G = gl + (b - s0) * S * S;
+            double nv[SL];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                const double* row = G + (lane_q * SL + j) * S;
+                double acc = 0.0;
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    const double xc = __shfl(v[c % SL], (threadIdx.x & ~(L - 1)) + c / SL, 64);
+                    acc = fma(row[c], xc, acc);
+                }
+                nv[j] = acc;
+            }
+            double m = 0.0;
+#pragma unroll
+            for (int j = 0; j < SL; ++j) m = fmax(m, nv[j]);
+            const double sc = 1.0 / wave_max(m);
+            double* dst = dst0 + (b - s0) * S * S;
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                v[j] = nv[j] * sc;
+                dst[(lane_q * SL + j) * S + q] = v[j];
+            }
+        }
+    } else {                                                     // rows: y^T <- y^T G_b
+        double* dst0 = SG + blockIdx.y * sstride + blockIdx.x * (long long)kScanC * S * S;
+        for (long long b = s1 - 1; b >= s0; --b) {
+            const double* G = gl + (b - s0) * S * S;
+            double nv[SL];
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {                       // y_c = sum_r y_r G[r][c], c = lane_q*SL + j
+                const int c = lane_q * SL + j;
+                double acc = 0.0;
+#pragma unroll
+                for (int rr = 0; rr < S; ++rr) {
+                    const double yr = __shfl(v[rr % SL], (threadIdx.x & ~(L - 1)) + rr / SL, 64);
+                    acc = fma(yr, G[rr * S + c], acc);
+                }
+                nv[j] = acc;
+            }
+            double m = 0.0;
+#pragma unroll
+            for (int j = 0; j < SL; ++j) m = fmax(m, nv[j]);
+            const double sc = 1.0 / wave_max(m);
+            double* dst = dst0 + (b - s0) * S * S;
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                v[j] = nv[j] * sc;
+                dst[q * S + lane_q * SL + j] = v[j];
+            }
+        }
+    }
+}
+
+// Windows: 16 lanes per window (one matrix row each; the whole vector in every lane) ->
+// filtered vector -> collapsed onto the asset's unique vols (sum_forecast_by_state,
+// msm_estimation.py:205-248, Q14: states in order) straight into fbs[t][d][u].  The window's
+// factors (<= 4 for n_in >> B C, their addresses known up front) are loaded one ahead.
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_scanwin(const double* __restrict__ Pre, long long pstride,
+                                                     const double* __restrict__ Suf1, long long ustride,
+                                                     const double* __restrict__ Gf, long long gstride,
+                                                     const double* __restrict__ PG, const double* __restrict__ SG,
+                                                     long long sstride, long long nfull, long long n_in, long long T,
+                                                     StateMapQ M, int dim, double* __restrict__ fbs) {
+    constexpr int S = 1 << K;
+    static_assert(S <= 16, "one matrix row per lane of a 16-lane group");
+    const int g = threadIdx.x % 16;
+    const long long t = (long long)blockIdx.x * (blockDim.x / 16) + threadIdx.x / 16;
+    const bool active = t < T;
+    const long long tt = active ? t : T - 1;
+    const int d = blockIdx.y;
+    Pre += d * pstride;
+    Suf1 += d * ustride;
+    Gf += d * gstride;
+    PG += d * sstride;
+    SG += d * sstride;
+    const int row = g < S ? g : 0;
+    const long long e = tt + n_in - 1;
+    const long long lo_b = tt / kScanB + 1, hi_b = e / kScanB - 1;   // full blocks strictly between
+    const long long sa = lo_b / kScanC, sb = hi_b / kScanC;
+    // the chain of factors applied to Suf_{b0}(t) u, first to last
+    int kind;                                                    // 0 none, 1 PG only, 2 SG only, 3 loose, 4 spread
+    long long cnt;
+    if (lo_b > hi_b) { kind = 0; cnt = 1; }
+    else if (sa == sb) {
+        const long long send = min(sa * kScanC + kScanC, nfull) - 1;
+        kind = lo_b == sa * kScanC ? 1 : (hi_b == send ? 2 : 3);
+        cnt = kind == 3 ? hi_b - lo_b + 2 : 2;
+    } else { kind = 4; cnt = (sb - sa + 1) + 1; }
+    auto mat = [&](long long k) -> const double* {
+        if (k == cnt - 1) return Pre + (e - (n_in - 1)) * S * S;
+        switch (kind) {
+            case 1: return PG + (sa * kScanC + (hi_b - sa * kScanC)) * S * S;
+            case 2: return SG + (sa * kScanC + (lo_b - sa * kScanC)) * S * S;
+            case 3: return Gf + (lo_b + k) * S * S;
+            default:
+                if (k == 0) return SG + (sa * kScanC + (lo_b - sa * kScanC)) * S * S;
+                if (k == cnt - 2) return PG + (sb * kScanC + (hi_b - sb * kScanC)) * S * S;
+                return SG + ((sa + k) * kScanC) * S * S;      // full superblock sa + k
+        }
+    };
+    double x[S];
+    {
+        double tot = 0.0;
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            x[c] = Suf1[tt * S + c];                             // Suf_{b0}(t) u, up to a factor
+            tot += x[c];
+        }
+        const double inv = 1.0 / tot;
+#pragma unroll
+        for (int c = 0; c < S; ++c) x[c] *= inv;
+    }
+    double cur[S], nxt[S];
+    {
+        const double* m0 = mat(0) + row * S;
+#pragma unroll
+        for (int c = 0; c < S; ++c) cur[c] = m0[c];
+    }
+    for (long long k = 0; k < cnt; ++k) {
+        if (k + 1 < cnt) {
+            const double* m1 = mat(k + 1) + row * S;
+#pragma unroll
+            for (int c = 0; c < S; ++c) nxt[c] = m1[c];
+        }
+        double y = 0.0;
+#pragma unroll
+        for (int c = 0; c < S; ++c) y = fma(cur[c], x[c], y);
+        double tot = 0.0;
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            x[c] = __shfl(y, (threadIdx.x & ~15) + c, 64);
+            tot += x[c];
+        }
+        const double inv = 1.0 / tot;
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            x[c] *= inv;
+            cur[c] = nxt[c];
+        }
+    }
+    if (!active || g >= M.q) return;
+    double f = 0.0;
+#pragma unroll
+    for (int c = 0; c < S; ++c) f += M.u[d][c] == g ? x[c] : 0.0;
+    fbs[(t * dim + d) * M.q + g] = f;
+}
+
 // sum_forecast_by_state (msm_estimation.py:205-248, Q14) + compute_forecast_combinations
-// (:392-418, Q7) on the device: one thread per date t.  filt [dim][T][S] -> fbs [T][dim][q]
+// (:392-418, Q7) on the device.  filt [dim][T][S] -> fbs [T][dim][q]
 // (states collapsed onto their unique 1e-6-rounded vol, summed in state order) and
 // pi [T][q^dim] in the reference's xy-meshgrid product order (2-D: f0[a] f1[b];
 // 3-D: (f0[L1] f1[L2]) f2[L0]).
@@ -384,25 +696,34 @@ struct StateMap {
     uint8_t u[3][128];                             // unique-vol index of state s of asset d
 };
 
-__global__ void k_msm_tables(StateMap M, int dim, int S, int q, const double* __restrict__ filt, long long T,
-                             double* __restrict__ fbs, double* __restrict__ pi) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    double f[3][8];
-    for (int d = 0; d < dim; ++d) {
-        for (int u = 0; u < q; ++u) f[d][u] = 0.0;
-        const double* row = filt + ((long long)d * T + t) * S;
-        for (int s2 = 0; s2 < S; ++s2) f[d][M.u[d][s2]] += row[s2];
-        for (int u = 0; u < q; ++u) fbs[(t * dim + d) * q + u] = f[d][u];
-    }
-    double* pt = pi + t * (dim == 2 ? q * q : q * q * q);
+// One thread per output: k_msm_fbs, thread per (date, asset), the
+// states of its filtered vector summed onto their unique vols in state order; k_msm_pi,
+// thread per (date, combination), the product in the reference's meshgrid order.
+__global__ void k_msm_fbs(StateMap M, int dim, int S, int q, const double* __restrict__ filt, long long T,
+                          double* __restrict__ fbs) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= T * dim) return;
+    const long long t = idx / dim;
+    const int d = (int)(idx % dim);
+    double f[8];
+    for (int u = 0; u < q; ++u) f[u] = 0.0;
+    const double* row = filt + ((long long)d * T + t) * S;
+    for (int s2 = 0; s2 < S; ++s2) f[M.u[d][s2]] += row[s2];
+    for (int u = 0; u < q; ++u) fbs[(t * dim + d) * q + u] = f[u];
+}
+
+__global__ void k_msm_pi(int dim, int q, const double* __restrict__ fbs, long long T, double* __restrict__ pi) {
+    const int Q = dim == 2 ? q * q : q * q * q;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= T * Q) return;
+    const long long t = idx / Q;
+    const int l = (int)(idx % Q);
+    const double* f = fbs + t * dim * q;
     if (dim == 2) {
-        for (int a = 0; a < q; ++a)
-            for (int b = 0; b < q; ++b) pt[a * q + b] = f[0][a] * f[1][b];
+        pi[idx] = f[l / q] * f[q + l % q];
     } else {
-        for (int L0 = 0; L0 < q; ++L0)
-            for (int L1 = 0; L1 < q; ++L1)
-                for (int L2 = 0; L2 < q; ++L2) pt[(L0 * q + L1) * q + L2] = (f[0][L1] * f[1][L2]) * f[2][L0];
+        const int L0 = l / (q * q), L1 = (l / q) % q, L2 = l % q;
+        pi[idx] = (f[L1] * f[q + L2]) * f[2 * q + L0];
     }
 }
 
@@ -869,6 +1190,59 @@ int launch_blocked_k(int k, const MsmParamsN& P, int dim, const double* cond, lo
     return CVQ_OK;
 }
 
+// Transfer-matrix scan filter (k_msm_blkscan -> k_msm_supscan -> k_msm_scanwin): 2 <= k <= 4
+// (one wavefront per superblock scan) and windows longer than two blocks.
+bool msm_scan_ok(int k, long long n_in) {
+    static const bool on = !getenv("CVQ_MSM_SCAN") || atoi(getenv("CVQ_MSM_SCAN")) != 0;   // A/B switch
+    return on && k >= 2 && k <= 4 && n_in > 2 * kScanB;
+}
+
+struct ScanLayout {                 // doubles of each scan buffer, per asset
+    long long pre, suf, gf, sup, nfull, nsup;
+};
+ScanLayout scan_layout(int k, long long n_in, long long T) {
+    const long long S = 1LL << k, N = n_in + T - 1;
+    ScanLayout L;
+    L.nfull = N / kScanB;
+    L.nsup = (L.nfull + kScanC - 1) / kScanC;
+    L.pre = T * S * S;
+    L.suf = T * S;
+    L.gf = L.nfull * S * S;
+    L.sup = L.nsup * kScanC * S * S;
+    return L;
+}
+
+template <int K>
+void launch_scan(const MsmParamsN& P, const StateMapQ& MQ, int dim, const double* r, long long N, long long n_in,
+                 long long T, double* buf, double* fbs, int* err, hipStream_t stream) {
+    constexpr int S = 1 << K;
+    const ScanLayout L = scan_layout(K, n_in, T);
+    double* Pre = buf;
+    double* Suf1 = Pre + dim * L.pre;
+    double* Gf = Suf1 + dim * L.suf;
+    double* PG = Gf + dim * L.gf;
+    double* SG = PG + dim * L.sup;
+    const long long nblk = (N + kScanB - 1) / kScanB;
+    hipLaunchKernelGGL(k_msm_blkscan<K>, dim3((unsigned)nblk, (unsigned)dim, 2), dim3(4 * S), 0, stream, P, r, N,
+                       n_in, T, Pre, L.pre, Suf1, L.suf, Gf, L.gf, err);
+    if (L.nsup > 0)
+        hipLaunchKernelGGL(k_msm_supscan<K>, dim3((unsigned)L.nsup, (unsigned)dim, 2), dim3(4 * S), 0, stream, Gf,
+                           L.gf, L.nfull, PG, SG, L.sup);
+    hipLaunchKernelGGL(k_msm_scanwin<K>, dim3((unsigned)((T + 15) / 16), (unsigned)dim), dim3(256), 0, stream, Pre,
+                       L.pre, Suf1, L.suf, Gf, L.gf, PG, SG, L.sup, L.nfull, n_in, T, MQ, dim, fbs);
+}
+
+int launch_scan_k(int k, const MsmParamsN& P, const StateMapQ& MQ, int dim, const double* r, long long N,
+                  long long n_in, long long T, double* buf, double* fbs, int* err, hipStream_t stream) {
+    switch (k) {
+        case 2: launch_scan<2>(P, MQ, dim, r, N, n_in, T, buf, fbs, err, stream); break;
+        case 3: launch_scan<3>(P, MQ, dim, r, N, n_in, T, buf, fbs, err, stream); break;
+        default: launch_scan<4>(P, MQ, dim, r, N, n_in, T, buf, fbs, err, stream); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    return CVQ_OK;
+}
+
 template <int K>
 void launch_msm_ll(const MsmParams* P, long long B, const double* r, long long N, double* out) {
     constexpr int L = Quad<K>::L;
@@ -892,8 +1266,14 @@ int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, 
     CVQ_REQUIRE(doubles != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(dim >= 1 && dim <= 3 && k >= 1 && k <= 7 && n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "bad shape");
     const long long S = 1LL << k, N = n_in + T - 1;
-    const int B = msm_block_len(k, n_in);
-    const long long G = B ? dim * (N / B) * S * S : 0;      // blocked filter: full-block products
+    long long G;
+    if (msm_scan_ok(k, n_in)) {                            // scan filter: prefixes, suffixes, block / superblock products
+        const ScanLayout L = scan_layout(k, n_in, T);
+        G = dim * (L.pre + L.suf + L.gf + 2 * L.sup);
+    } else {
+        const int B = msm_block_len(k, n_in);
+        G = B ? dim * (N / B) * S * S : 0;                  // blocked filter: full-block products
+    }
     *doubles = dim * N * S + dim * T * S + G + 2;          // cond, filtered probabilities, [G], error word
     return CVQ_OK;
 }
@@ -921,19 +1301,36 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const long long N = n_in + T - 1;
-    const int B = msm_block_len(k, n_in);
+    const bool scan = msm_scan_ok(k, n_in);
+    const int B = scan ? 0 : msm_block_len(k, n_in);
     double* cond = scratch;
     double* filt = cond + (long long)dim * N * S;
     double* G = filt + (long long)dim * T * S;
-    int* err = (int*)(G + (B ? (long long)dim * (N / B) * S * S : 0));
+    long long gsz = B ? (long long)dim * (N / B) * S * S : 0;
+    if (scan) {
+        const ScanLayout L = scan_layout(k, n_in, T);
+        gsz = dim * (L.pre + L.suf + L.gf + 2 * L.sup);
+    }
+    int* err = (int*)(G + gsz);
     CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
-    hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,
-                       returns_c, N, cond);
-    if (B) rc = launch_blocked_k(k, P, dim, cond, N, n_in, T, B, G, filt, err, st);
-    else rc = launch_filter_k(k, P, dim, cond, N, n_in, T, filt, err, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_msm_tables, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, M, dim, S, q, filt, T,
-                       fbs_out, pi_out);
+    if (scan) {                        // densities computed per block inside; the collapse fused into the windows
+        StateMapQ MQ{};
+        MQ.q = q;
+        for (int d = 0; d < dim; ++d)
+            for (int s2 = 0; s2 < S; ++s2) MQ.u[d][s2] = M.u[d][s2];
+        rc = launch_scan_k(k, P, MQ, dim, returns_c, N, n_in, T, G, fbs_out, err, st);
+        if (rc) return rc;
+    } else {
+        hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,
+                           returns_c, N, cond);
+        if (B) rc = launch_blocked_k(k, P, dim, cond, N, n_in, T, B, G, filt, err, st);
+        else rc = launch_filter_k(k, P, dim, cond, N, n_in, T, filt, err, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_msm_fbs, dim3((unsigned)((T * dim + 255) / 256)), dim3(256), 0, st, M, dim, S, q, filt,
+                           T, fbs_out);
+    }
+    const long long Q = dim == 2 ? (long long)q * q : (long long)q * q * q;
+    hipLaunchKernelGGL(k_msm_pi, dim3((unsigned)((T * Q + 255) / 256)), dim3(256), 0, st, dim, q, fbs_out, T, pi_out);
     CVQ_HIP_CHECK(hipGetLastError());
     return CVQ_OK;
 }
@@ -941,8 +1338,14 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
 int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n_in, int64_t T, void* stream) {
     CVQ_REQUIRE(scratch != nullptr, CVQ_ERR_INVALID, "NULL argument");
     const long long S = 1LL << k, N = n_in + T - 1;
-    const int B = msm_block_len(k, n_in);
-    const long long G = B ? dim * (N / B) * S * S : 0;
+    long long G;
+    if (msm_scan_ok(k, n_in)) {
+        const ScanLayout L = scan_layout(k, n_in, T);
+        G = dim * (L.pre + L.suf + L.gf + 2 * L.sup);
+    } else {
+        const int B = msm_block_len(k, n_in);
+        G = B ? dim * (N / B) * S * S : 0;
+    }
     int e = 0;
     CVQ_HIP_CHECK(hipMemcpyAsync(&e, scratch + dim * N * S + dim * T * S + G, sizeof(int), hipMemcpyDeviceToHost,
                                  (hipStream_t)stream));

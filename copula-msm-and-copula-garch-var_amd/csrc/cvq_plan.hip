@@ -107,6 +107,7 @@ int make_tconst(double nu, TConst* tk, double** d_cf) {
     return CVQ_OK;
 }
 
+int compact_tail_cap();                      // cvq_compact.hip: the block tail's node capacity
 }  // namespace cvq
 
 using namespace cvq;
@@ -156,8 +157,11 @@ struct cvq_plan {
     double cut_key[6] = {0, 0, 0, 0, 0, 0};
     bool cut_valid = false;
     std::vector<double> hvc;     // every v*(r, j >= 1), sorted (the bisection cells' node counts)
-    int* d_ccount = nullptr;     // [4][1 << ccount_depth] cell node counts (nullptr: counted on device)
+    int* d_ccount = nullptr;     // [4][2 << ccount_depth] cell node counts (nullptr: counted on device)
     int ccount_depth = -1;
+    uint32_t* d_tlist = nullptr; // [n (n - 1)] nodes (r, j >= 1) in hvc's order: the block tail's list
+    double* d_tvs = nullptr;     // [n (n - 1)] = hvc on the device
+    int bstart[4] = {0, 0, 0, 0};   // ub(bracket lower) in hvc for the cached solve arguments
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -391,9 +395,11 @@ double vstar_exact(double xj, double lev, double w0) {
         for (; steps < 64 && !pred(v); ++steps) v = std::nextafter(v, HUGE_VAL);
     }
     if (steps < 64) return v;
+    // ordered-integer bisection (cancellation near 0: v* is ~ -ulp(lev) / 2, far below the
+    // start's ulp); the span of the ordered range exceeds INT64_MAX, so distances are unsigned
     int64_t lo = d2o(-HUGE_VAL), hi = d2o(HUGE_VAL);           // pred(lo) false, pred(hi) true
-    while (hi - lo > 1) {
-        const int64_t m = lo + (hi - lo) / 2;
+    while ((uint64_t)hi - (uint64_t)lo > 1) {
+        const int64_t m = (int64_t)((uint64_t)lo + ((uint64_t)hi - (uint64_t)lo) / 2);
         if (pred(o2d(m))) hi = m; else lo = m;
     }
     return o2d(hi);
@@ -676,11 +682,14 @@ void build_buckets(const std::vector<double>& x, std::vector<int16_t>& bk, doubl
 
 // COMPACT: node counts of the bisection cells -- heap node h of bracket b's tree holds
 // #{(r, j >= 1): lo_h < v*(r, j) <= hi_h}, with the device's mids (lo + hi) / 2 -- for
-// every depth above the first one whose cells all hold <= kTailCap nodes.  The kernel
-// enters its one-wave tail from this table instead of reducing bracket node counts at
-// every level.  depth = -1: no such depth <= kCompactMaxDepth (the kernel counts).
+// every depth down to D, the first depth >= 1 whose cells all hold <= cap nodes (table
+// [4][2 << D], heap nodes 1 .. 2^(D+1) - 1).  The kernel leaves its workgroup levels for
+// the block tail from this table (a cell's sorted positions follow from the counts)
+// instead of reducing bracket node counts at every level.  depth = -1: no such depth
+// <= kCompactMaxDepth (the kernel counts and runs its one-wave tail).
 constexpr int kCompactMaxDepth = 16;
-void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, std::vector<int>& cc, int* depth) {
+void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, int cap, std::vector<int>& cc,
+                       int* depth) {
     const double br[4][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.sg1, P.vmax}, {P.fg, P.sg1}};   // k_compact's brackets
     std::vector<std::vector<int>> cnt;                      // cnt[d][(b << d) + k]: depth-d cell k of bracket b
     std::vector<double> lo(4), hi(4);
@@ -691,10 +700,10 @@ void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, std::
         bool small = true;
         for (size_t e = 0; e < lo.size(); ++e) {
             c[e] = std::max(host_ub(vs, hi[e]) - host_ub(vs, lo[e]), 0);
-            small = small && c[e] <= kTailCap;
+            small = small && c[e] <= cap;
         }
-        if (small) { *depth = d; break; }
         cnt.push_back(c);
+        if (small && d >= 1) { *depth = d; break; }
         std::vector<double> l2(2 * lo.size()), h2(2 * lo.size());
         for (size_t e = 0; e < lo.size(); ++e) {            // children 2k (lower half), 2k + 1 (upper half)
             const double mid = (lo[e] + hi[e]) / 2;
@@ -707,10 +716,11 @@ void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, std::
     cc.clear();
     if (*depth < 0) return;
     const int D = *depth;
-    cc.assign((size_t)4 << D, 0);
-    for (int d = 0; d < D; ++d)
+    cc.assign((size_t)4 << (D + 1), 0);
+    for (int d = 0; d <= D; ++d)
         for (int b = 0; b < 4; ++b)
-            for (int k = 0; k < (1 << d); ++k) cc[((size_t)b << D) + (1 << d) + k] = cnt[d][((size_t)b << d) + k];
+            for (int k = 0; k < (1 << d); ++k)
+                cc[((size_t)b << (D + 1)) + (1 << d) + k] = cnt[d][((size_t)b << d) + k];
 }
 
 // Fixed-level cut table (and the bisection cells' node counts) for the cached solve arguments.
@@ -727,7 +737,9 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     if (!p->d_cutfix) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cutfix, h.size() * sizeof(int16_t)));
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cutfix, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
     std::vector<int> cc;
-    build_cell_counts(p->hvc, P, cc, &p->ccount_depth);
+    build_cell_counts(p->hvc, P, compact_tail_cap(), cc, &p->ccount_depth);
+    const double blo[4] = {P.vmin, P.sg0, P.sg1, P.fg};      // k_compact's brackets' lower levels
+    for (int b = 0; b < 4; ++b) p->bstart[b] = host_ub(p->hvc, blo[b]);
     static const bool no_cc = getenv("CVQ_COMPACT_COUNT") && atoi(getenv("CVQ_COMPACT_COUNT")) != 0;   // A/B switch
     if (no_cc) p->ccount_depth = -1;
     if (p->ccount_depth >= 0) {
@@ -781,11 +793,11 @@ namespace cvq {
 int compact_max_n();                                                                  // cvq_compact.hip
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,
-                   double* snaps, Header* hdr, int* defer, bool generic);
+                   double* snaps, Header* hdr, int* defer, bool generic, size_t abi);
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
                   const double* bounds, double* out, double* snaps, Header* hdr, double* stamps,
-                  bool sweep);                                                        // cvq_sorted.hip
+                  bool sweep, size_t abi);                                            // cvq_sorted.hip
 }
 namespace {
 
@@ -821,7 +833,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         return launch_sorted(p->S, P, sorted_geom(p, true), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
                              direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
                              dbg_stamps ? (double*)p->d_stamps : nullptr,
-                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok);
+                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok, kernel_abi_key() ^ (sizeof(SortedGeom) << 40));
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
@@ -835,10 +847,12 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
             CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
             p->capDefer = p->T + 2;
         }
+        const bool tab = p->ccount_depth >= 0;
         const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
-                            p->ccount_depth >= 0 ? p->d_ccount : nullptr, p->ccount_depth};
+                            tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
+                            {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]}};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
-                              snaps, hdr, p->d_defer, !p->fast_hint);
+                              snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
         // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
@@ -869,7 +883,8 @@ int launch_slab(cvq_plan* p, const double* bounds, double* out) {
     if (sorted_family(p)) {
         SolveConst P{};
         return launch_sorted(p->S, P, sorted_geom(p, false), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
-                             direct_fused(p), 1, bounds, out, nullptr, nullptr, nullptr, false);
+                             direct_fused(p), 1, bounds, out, nullptr, nullptr, nullptr, false,
+                             kernel_abi_key() ^ (sizeof(SortedGeom) << 40));
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {      // COMPACT: slabs of arbitrary bounds run k_direct
         SolveConst P{};
@@ -1112,6 +1127,11 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     S.Q = Q;
     S.nrows = s->dim == 2 ? s->n : s->n * s->n;
     S.w0 = s->weights[0];
+    {   // exact reciprocal: w0 = 2^e (frexp mantissa 1/2) and 1/w0 a normal double
+        int e2 = 0;
+        const double m2 = std::frexp(s->weights[0], &e2);
+        S.w0_inv = (m2 == 0.5 && std::isnormal(1.0 / s->weights[0])) ? 1.0 / s->weights[0] : 0.0;
+    }
     S.w1 = s->weights[1];
     S.w2 = s->dim == 3 ? s->weights[2] : 0.0;
 
@@ -1236,9 +1256,26 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         build_vstar(p->hx, S.w0, S.w1, vs);
         p->hvc.clear();
         p->hvc.reserve((size_t)n * (n - 1));
+        // COMPACT's nodes: j >= 1 (Q9), sorted by v* (ties by (r, j)): hvc and the block tail's list
+        std::vector<uint32_t> ord;
+        ord.reserve((size_t)n * (n - 1));
         for (int r = 0; r < n; ++r)
-            for (int j = 1; j < n; ++j) p->hvc.push_back(vs[(size_t)r * n + j]);   // COMPACT's nodes: j >= 1 (Q9)
-        std::sort(p->hvc.begin(), p->hvc.end());
+            for (int j = 1; j < n; ++j) ord.push_back((uint32_t)(r * n + j));
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return vs[a] < vs[b]; });
+        std::vector<uint32_t> tl(ord.size());
+        for (size_t i = 0; i < ord.size(); ++i) {
+            p->hvc.push_back(vs[ord[i]]);
+            const uint32_t r = ord[i] / n, j = ord[i] % n;
+            const bool gend = i + 1 == ord.size() || !(vs[ord[i + 1]] == vs[ord[i]]);
+            tl[i] = r | (j << kTlColShift) | (gend ? kTlGroupEnd : 0u);
+        }
+        if ((rc = dev_alloc(&p->d_tlist, tl.size())) || (rc = dev_alloc(&p->d_tvs, p->hvc.size()))) {
+            cvq_plan_destroy(p);
+            return rc;
+        }
+        e = hipMemcpy(p->d_tlist, tl.data(), tl.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_tvs, p->hvc.data(), p->hvc.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
         std::vector<int16_t> bk;
         build_buckets(p->hx, bk, &p->bx0, &p->binv);
         p->nb = (int)bk.size();
@@ -1263,7 +1300,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);

@@ -86,7 +86,10 @@ void launch_c(const SortedLaunch& L) {
 
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
-                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps, bool sweep) {
+                  const double* bounds, double* out, double* snaps, Header* hdr, double* stamps, bool sweep,
+                  size_t abi) {
+    CVQ_REQUIRE(abi == (kernel_abi_key() ^ (sizeof(SortedGeom) << 40)), CVQ_ERR_STATE,
+                "libcvq objects built from different headers (rebuild all)");
     CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
     const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
     switch (S.copula) {

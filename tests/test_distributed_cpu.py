@@ -37,7 +37,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, batches=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -64,18 +64,31 @@ def _worker(rank, world, port, case, q):
             assert not err
             var.copy_(torch.from_numpy(v))
 
-        s = ShardedVaR(T, K + 1, local, finalize, torch.device("cpu"))
-        var = s.solve().numpy().copy()
-        q.put((rank, var))
+        if batches == 1:
+            s = ShardedVaR(T, K + 1, local, finalize, torch.device("cpu"))
+            var = s.solve().numpy().copy()
+            q.put((rank, var))
+        else:
+            # bench.py's in-flight batches: one process group (communicator) per batch, the
+            # batches' solves interleaved in step order i % batches
+            groups = [dist.new_group(list(range(world))) for _ in range(batches)]
+            shs = []
+            for g in groups:
+                s = ShardedVaR(T, K + 1, local, finalize, torch.device("cpu"), group=g)
+                shs.append(s)
+            out = []
+            for i in range(2 * batches):
+                out.append(shs[i % batches].solve().numpy().copy())
+            q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-def _run(case, world):
+def _run(case, world, batches=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, batches)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
@@ -119,3 +132,14 @@ def test_gloo_world3_uneven_blocks():
     out = _run("msm_gauss_n64", 3)
     for var in out.values():
         assert np.array_equal(var, z["var"])
+
+
+def test_gloo_world2_three_batches_own_groups():
+    """Three in-flight batches (bench.py --inflight 3), each with its own process group, their
+    all-gathers interleaved: every solve on every rank is bit-identical to the reference."""
+    z = load_golden("cfg1")
+    out = _run("cfg1", 2, batches=3)
+    for r, vs in out.items():
+        assert len(vs) == 6
+        for var in vs:
+            assert np.array_equal(var, z["var"])

@@ -169,3 +169,20 @@ def test_blocked_filter_matches_stepwise(n_in, T):
         smap, _ = tables.unique_vol_map(vs[None, :])
         ref = np.stack([seq[:, smap[0] == u].sum(axis=1) for u in range(fbs.shape[2])], axis=1)
         np.testing.assert_allclose(fbs[:, d, :], ref, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize("n_in,T", [(65, 1), (70, 50), (100, 17), (600, 300), (1135, 1000), (1135, 7)])
+def test_scan_filter_window_shapes(n_in, T):
+    """cvq_msm_tables' transfer-matrix scan (block prefixes / suffixes, superblock scans, <= 5
+    mat-vecs per window) against the step-by-step filter behind the host assembly, over window
+    lengths that hit every middle-block case (none, a superblock prefix or suffix alone, loose
+    blocks inside one superblock, several superblocks) and T from 1 to 1000."""
+    from copula_var import synthetic, tables
+    c = synthetic.baseline_configs()[2].with_(T=T, n_in=n_in)
+    rets = synthetic.simulate_returns(c)
+    _, _, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
+    (fbs, pi), uvs, _ = tables.msm_integration_params(centred, c.n_in, c.msm_params, c.k, c.num_points)
+    mt, uvs_d, _ = _device_tables(centred[:-1], c.n_in, c.k, c.msm_params)
+    np.testing.assert_array_equal(uvs_d, uvs)
+    np.testing.assert_allclose(mt.fbs.cpu().numpy(), fbs, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(mt.pi.cpu().numpy(), pi, rtol=1e-12, atol=1e-300)

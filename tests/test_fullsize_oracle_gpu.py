@@ -172,3 +172,33 @@ def test_fast_path_proof_boundary_sigma_xmax_over_6_nu1():
         p.close()
     assert it == ref_it
     assert np.array_equal(var, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("case", ["cfg1", "cfg5_n64", "cfg4_k4_n16", "cfg3_n128"])
+@pytest.mark.parametrize("strategy", ["sorted", "prefix", "compact"])
+def test_slabs_ending_at_zero(case, strategy):
+    """Slabs whose upper bound is 0 (the default v_cap): the nodes on the anti-diagonal have
+    v* ~ -ulp(level) / 2, found by the host's ordered-integer bisection (vstar_exact); a
+    signed overflow there once sent them to +inf, so SORTED dropped them from every slab
+    ending at 0 (a solve never reaches them)."""
+    from conftest import load_golden
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem
+    z = load_golden(case)
+    if strategy == "compact" and int(z["dim"]) != 2:
+        pytest.skip("COMPACT is 2-D")
+    msm = str(z["model"]) == "msm"
+    vs = z.get("unique_vol_states")
+    per = (z["forecasts_by_states"], z["forecasts"]) if msm else z["sigma_forecasts"]
+    P = Problem(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+                z["combos"], z["weights"], z["copula_params"], per, vs)
+    p = QuadraturePlan(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+                       z["combos"], z["weights"], z["copula_params"], vol_states=vs, strategy=strategy)
+    try:
+        p.set_dates(per if msm else [per])
+        for b in ([-1e-15, 0.0], [-0.1, 0.0], [-2.0, 0.0], [-100.0, 0.0]):
+            bounds = np.tile(b, (P.T, 1))
+            np.testing.assert_allclose(p.compute_integral(bounds), P.compute_integral(bounds), rtol=SLAB_RTOL,
+                                       atol=SLAB_ATOL, err_msg=f"{case} {strategy} {b}")
+    finally:
+        p.close()

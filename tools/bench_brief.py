@@ -4,4 +4,8 @@ import sys
 
 d = json.loads(sys.stdin.read().strip().splitlines()[-1])
 k = {n: round(v["avg_us"], 1) for n, v in d["kernels"].items()}
-print(round(d["value"]), round(d["ms_per_step"] * 1e3, 1), "us/step", d["var_checksum"], d["var_nan"], k)
+ss = d.get("single_solve") or {}
+rf = d.get("roofline") or {}
+print(round(d["value"]), round(d["ms_per_step"] * 1e3, 1), "us/step", "single", round(ss.get("value", 0)),
+      "fp64", round(rf.get("frac", 0), 4), "launch_us", round(rf.get("avg_launch_us", 0), 1), d["var_checksum"],
+      d["var_nan"], k)

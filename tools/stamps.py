@@ -42,6 +42,20 @@ if STRAT == "compact" and (st[:, 27] != 0).any():
         m = per_wg == c
         print(f"  WGs on a CU with {c} dates: {m.sum():5d}  duration mean {dur[m].mean():7.0f}  max {dur[m].max():7.0f}"
               f" (10 ns ticks)")
+    # arrival order of each workgroup on its CU (0 = first started) vs duration: the SIMD
+    # arbitration favours older waves
+    t0 = st[:, 25].astype(np.float64)
+    order = np.zeros(T, dtype=int)
+    for k in range(uk.size):
+        idx = np.nonzero(inv == k)[0]
+        order[idx[np.argsort(t0[idx], kind="stable")]] = np.arange(idx.size)
+    print("  duration by arrival order on the CU:",
+          " ".join(f"#{o}: {dur[order == o].mean():.0f}" for o in np.unique(order)))
+    # by bracket class of the solved VaR (calc_var_class.py:137-149): (<-3.5], (-3.5,-3], (-3,-2], (-2,0]
+    v = var - ptf
+    cls = np.digitize(v, [-3.5, -3.0, -2.0])
+    print("  duration by VaR bracket (<-3.5, -3.5..-3, -3..-2, -2..0):",
+          " ".join(f"{dur[cls == c].mean():.0f} (n={int((cls == c).sum())})" for c in range(4) if (cls == c).any()))
 if STRAT == "direct":
     names = ["tables", "rowsetup", "slab1", "slab2", "bracket"] + [f"it{i}" for i in range(it)]
     cols = list(range(6 + it))

@@ -1,0 +1,51 @@
+"""Split a rocprofv3 kernel trace of one bench.py run into its legs (GPU-box tool).
+
+bench.py runs, in order: the in-flight leg (warmup + steps launches of the dominant
+kernel), the single-solve leg (warmup + steps, one batch at a time), then the e2e leg
+(warmup + steps).  The dominant kernel's dispatches, in start-time order, are cut
+accordingly and each leg's average kernel duration is printed -- the single-solve leg's
+average is what bench.py's HIP events time for "roofline".
+
+usage: python tools/trace_legs.py <dir with *kernel_trace.csv> [--steps 100 --warmup 5 --kernel k_compact]
+"""
+import csv
+import glob
+import os
+import sys
+
+
+def arg(name, default):
+    return type(default)(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
+
+
+def main():
+    root = sys.argv[1]
+    steps, warmup = arg("--steps", 100), arg("--warmup", 5)
+    kern = arg("--kernel", "k_compact")
+    files = glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no kernel_trace.csv under {root}")
+    rows = []
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            name = r.get("Kernel_Name", "")
+            if kern in name and "true>(" not in name:                     # k_compact: the fast instance (GEN = false)
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    per = warmup + steps
+    legs = [("inflight", 0), ("single_solve", per), ("e2e", 2 * per)]
+    print(f"{len(rows)} dispatches of {kern} (fast instance); legs of {per} = {warmup} warmup + {steps} timed")
+    for nm, off in legs:
+        seg = rows[off + warmup: off + per]
+        if not seg:
+            continue
+        d = [(e - s) / 1e3 for s, e, _ in seg]
+        span = (seg[-1][1] - seg[0][0]) / 1e3
+        print(f"  {nm:13s} launches {len(d):4d}  avg {sum(d) / len(d):8.2f} us  min {min(d):8.2f}  max {max(d):8.2f}"
+              f"  first-start..last-end {span:9.1f} us")
+    if rows:
+        print(f"  kernel: {rows[0][2][:160]}")
+
+
+if __name__ == "__main__":
+    main()
