@@ -23,10 +23,10 @@ Prints ONE JSON line (rank 0).
   roofline     -- dominant kernel (k_compact / k_sorted / k_mass), bound "fp64-valu":
                   algorithmic FP64 work (SURVEY.md §8d convention: FLOP per reachable
                   node x reachable nodes x dates per launch) / the kernel's average
-                  duration, timed with HIP events on its stream in the single-solve leg
-                  (one launch in flight, so the bracket is the kernel's own duration, as
+                  duration, timed with HIP events on its stream in a separate one-batch
+                  leg (one launch in flight, so the bracket is the kernel's own duration, as
                   rocprofv3's kernel trace gives it; profiles/ holds the trace split by
-                  leg).  Sub-object "hbm": 8 B x reachable nodes per date (the judged
+                  leg).  The legs that give value / single_solve carry no events.  Sub-object "hbm": 8 B x reachable nodes per date (the judged
                   algorithmic bytes of §8d) over the same duration, and the PMC traffic.
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
@@ -194,22 +194,29 @@ def main():
         return el, kt
 
     dom = "mass" if a.strategy == "prefix" else "solve"                      # dominant kernel
-    elapsed, kt = timed(nf, a.steps, a.warmup, True if a.time_all else (dom,))
+    # the timed legs carry no HIP events (an event record between two launches on a stream
+    # delays the second: rocprofv3 saw ~10 us gaps in an event-timed one-batch leg); the
+    # dominant kernel's duration comes from a separate event-timed leg below
+    elapsed, kt = timed(nf, a.steps, a.warmup, True if a.time_all else None)
     vals = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
     ms_step = elapsed / a.steps * 1e3
     value = T_total * a.steps / elapsed
     if nf > 1 and a.single:
-        el1, kt1 = timed(1, a.steps, a.warmup, (dom,))                        # one batch at a time
+        el1, _ = timed(1, a.steps, a.warmup, None)                            # one batch at a time
         v1 = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
         assert np.array_equal(v1, vals, equal_nan=True), "single-solve leg changed the VaR"
     else:
-        el1, kt1 = elapsed, kt
+        el1 = elapsed
     single = {"value": T_total * a.steps / el1, "unit": "VaR-dates/s", "ms_per_step": el1 / a.steps * 1e3,
               "inflight": 1, "steps": a.steps,
               "scope": "one calc_var-equivalent solve per step (utils/calc_var_class.py:109-175), tables resident"}
 
-    # roofline of the dominant kernel from the single-solve leg: one launch in flight, so the
-    # HIP events bracket the kernel's own duration (rocprofv3 kernel trace: profiles/)
+    # roofline of the dominant kernel: one batch at a time with HIP events around each
+    # launch, so an event pair brackets the kernel's own duration (rocprofv3 kernel trace
+    # of the same leg: profiles/, tools/trace_legs.py)
+    el_r, kt1 = timed(1, a.steps, a.warmup, (dom,))
+    for p in plans:
+        p.enable_timing(False)
     dom_ms, dom_n = kt1[dom]
     dom_avg_s = dom_ms / max(dom_n, 1) / 1e3
     # FP64 basis: per reachable node 14 FLOP + 1 pow (counted as 1) for Student
@@ -267,7 +274,9 @@ def main():
                          "flop_per_node": flop_node, "reach_nodes_per_date": plan.reach_nodes,
                          "dates_per_launch": per, "flop_per_launch": flop_launch,
                          "avg_launch_us": dom_avg_s * 1e6, "launches": dom_n,
-                         "timing": "HIP events on the kernel's stream, single-solve leg (one launch in flight)",
+                         "timing": "HIP events on the kernel's stream, a separate one-batch leg (one launch in "
+                                   "flight); the timed legs carry no events",
+                         "event_leg_ms_per_step": el_r / a.steps * 1e3,
                          "hbm": {"alg_bytes_per_launch": alg_bytes, "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                                  "pmc_bytes_per_launch": traffic}},

@@ -4,9 +4,10 @@
 set -e
 name=$1; shift
 cd "$(dirname "$0")/../copula-msm-and-copula-garch-var_amd"
+flock /tmp/cvq_make.lock make -s   # every base object up to date
 out=../build_variants/$name
 mkdir -p $out
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function "$@" \
     -c csrc/cvq_sorted.hip -o $out/cvq_sorted.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libcvq.so build/cvq_plan.o build/cvq_forecast.o \
-    build/cvq_compact.o $out/cvq_sorted.o
+    build/cvq_compact.o build/cvq_ci_*.o $out/cvq_sorted.o

@@ -1,12 +1,14 @@
 """Split a rocprofv3 kernel trace of one bench.py run into its legs (GPU-box tool).
 
 bench.py runs, in order: the in-flight leg (warmup + steps launches of the dominant
-kernel), the single-solve leg (warmup + steps, one batch at a time), then the e2e leg
-(warmup + steps).  The dominant kernel's dispatches, in start-time order, are cut
-accordingly and each leg's average kernel duration is printed -- the single-solve leg's
+kernel), the single-solve leg (warmup + steps, one batch at a time), the event-timed
+roofline leg (the same, with HIP events), then the e2e leg (warmup + steps).  The
+dominant kernel's dispatches, in start-time order, are cut accordingly and each leg's
+average kernel duration and launch-to-launch gap are printed -- the roofline leg's
 average is what bench.py's HIP events time for "roofline".
 
-usage: python tools/trace_legs.py <dir with *kernel_trace.csv> [--steps 100 --warmup 5 --kernel k_compact]
+usage: python tools/trace_legs.py <dir with *kernel_trace.csv> [--steps 100 --warmup 5 --kernel k_compact
+       --legs inflight,single_solve,roofline,e2e]
 """
 import csv
 import glob
@@ -33,7 +35,8 @@ def main():
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
     per = warmup + steps
-    legs = [("inflight", 0), ("single_solve", per), ("e2e", 2 * per)]
+    names = arg("--legs", "inflight,single_solve,roofline,e2e").split(",")
+    legs = [(nm, i * per) for i, nm in enumerate(names)]
     print(f"{len(rows)} dispatches of {kern} (fast instance); legs of {per} = {warmup} warmup + {steps} timed")
     for nm, off in legs:
         seg = rows[off + warmup: off + per]
@@ -41,8 +44,10 @@ def main():
             continue
         d = [(e - s) / 1e3 for s, e, _ in seg]
         span = (seg[-1][1] - seg[0][0]) / 1e3
+        gaps = [(seg[i + 1][0] - seg[i][1]) / 1e3 for i in range(len(seg) - 1)]
+        gap = f"  mean end->next start {sum(gaps) / len(gaps):7.2f} us" if gaps else ""
         print(f"  {nm:13s} launches {len(d):4d}  avg {sum(d) / len(d):8.2f} us  min {min(d):8.2f}  max {max(d):8.2f}"
-              f"  first-start..last-end {span:9.1f} us")
+              f"  first-start..last-end {span:9.1f} us{gap}")
     if rows:
         print(f"  kernel: {rows[0][2][:160]}")
 
