@@ -163,9 +163,11 @@ def main():
             else:
                 shardeds[k].solve(check=False)
 
-    def timed(n_batches, steps, warmup, timing=None):
+    def timed(n_batches, steps, warmup, timing=None, bracket=None):
         """Wall time of `steps` steps (batch i % n_batches), barrier + synchronize on both
-        sides, max over ranks."""
+        sides, max over ranks.  bracket: a list that receives the device time (ms) between
+        two HIP events recorded on batch 0's stream before the first and after the last
+        step (no events between launches)."""
         for i in range(warmup):
             step_fn(i % n_batches)
         torch.cuda.synchronize()
@@ -174,10 +176,17 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        if bracket is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(streams[0])
         t0 = time.perf_counter()
         for i in range(steps):
             step_fn(i % n_batches)
+        if bracket is not None:
+            ev1.record(streams[0])
         torch.cuda.synchronize()
+        if bracket is not None:
+            bracket.append(ev0.elapsed_time(ev1))
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
@@ -194,34 +203,59 @@ def main():
         return el, kt
 
     dom = "mass" if a.strategy == "prefix" else "solve"                      # dominant kernel
-    # the timed legs carry no HIP events (an event record between two launches on a stream
-    # delays the second: rocprofv3 saw ~10 us gaps in an event-timed one-batch leg); the
-    # dominant kernel's duration comes from a separate event-timed leg below
-    elapsed, kt = timed(nf, a.steps, a.warmup, True if a.time_all else None)
+    # no HIP events between the timed legs' launches (an event record between two launches on
+    # a stream delays the second: rocprofv3 saw ~10 us gaps in an event-timed one-batch leg)
+    brk0 = []                                         # one batch in flight: the main leg's bracket
+    elapsed, kt = timed(nf, a.steps, a.warmup, True if a.time_all else None, brk0 if nf == 1 else None)
     vals = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
     ms_step = elapsed / a.steps * 1e3
     value = T_total * a.steps / elapsed
+    # one batch at a time; its back-to-back launches bracketed by two HIP events on the stream
+    # (the step is the one fused solve kernel for COMPACT / SORTED / SWEEP: the bracket over
+    # K steps / K is the kernel's average duration, as rocprofv3's kernel trace gives it)
+    one_kernel = a.strategy in ("compact", "sorted", "sweep") and not sharded
+    brk = []
     if nf > 1 and a.single:
-        el1, _ = timed(1, a.steps, a.warmup, None)                            # one batch at a time
+        el1, _ = timed(1, a.steps, a.warmup, None, brk)
         v1 = (vars_[0] if not sharded else shardeds[0].var).cpu().numpy()
         assert np.array_equal(v1, vals, equal_nan=True), "single-solve leg changed the VaR"
     else:
         el1 = elapsed
+        brk = brk0
     single = {"value": T_total * a.steps / el1, "unit": "VaR-dates/s", "ms_per_step": el1 / a.steps * 1e3,
               "inflight": 1, "steps": a.steps,
               "scope": "one calc_var-equivalent solve per step (utils/calc_var_class.py:109-175), tables resident"}
 
-    # roofline of the dominant kernel: one batch at a time with HIP events around each
-    # launch, so an event pair brackets the kernel's own duration (rocprofv3 kernel trace
-    # of the same leg: profiles/, tools/trace_legs.py)
-    el_r, kt1 = timed(1, a.steps, a.warmup, (dom,))
+    # roofline of the dominant kernel.  COMPACT / SORTED / SWEEP: the single-solve leg's event
+    # bracket / K.  Otherwise (several kernels per step): one batch at a time with HIP events
+    # around each launch of the dominant kernel.
+    if one_kernel and brk:
+        el_r, kt1 = el1, {dom: (brk[0], a.steps)}
+        timing_note = ("two HIP events on the kernel's stream bracketing the single-solve leg's K back-to-back "
+                       "launches (no events between launches); avg = bracket / K")
+    else:
+        el_r, kt1 = timed(1, a.steps, a.warmup, (dom,))
+        timing_note = "HIP events around each launch on the kernel's stream, a separate one-batch leg"
     for p in plans:
         p.enable_timing(False)
     dom_ms, dom_n = kt1[dom]
     dom_avg_s = dom_ms / max(dom_n, 1) / 1e3
-    # FP64 basis: per reachable node 14 FLOP + 1 pow (counted as 1) for Student
+    # FP64 basis (SURVEY §8d convention): per node 14 FLOP + 1 pow (counted as 1) for Student,
+    # over the nodes the solve evaluates -- counted on the device in one extra, untimed solve
+    # (SORTED evaluates each node of its bisection path once: cfg 4 ~17% of the reachable set,
+    # so the reachable-node basis would overstate the work), the reachable-node figure beside it
     flop_node = {"student": 15.0, "gaussian": 14.0, "plackett": 16.0}[c.copula] + (9.0 if c.dim == 3 else 0.0)
-    flop_launch = flop_node * plan.reach_nodes * per
+    nodes_eval = None
+    if a.strategy in ("compact", "sorted", "sweep") and not sharded:
+        plan.count_nodes(True)
+        step_fn(0)
+        torch.cuda.synchronize()
+        nodes_eval = plan.nodes_evaluated()
+        plan.count_nodes(False)
+        v2 = vars_[0].cpu().numpy()
+        assert np.array_equal(v2, vals, equal_nan=True), "node-count solve changed the VaR"
+    flop_launch = flop_node * (nodes_eval if nodes_eval is not None else plan.reach_nodes * per)
+    flop_reach = flop_node * plan.reach_nodes * per
     fp64_tflops = flop_launch / dom_avg_s / 1e12 if dom_avg_s > 0 else 0.0
     alg_bytes = 8.0 * plan.reach_nodes * per          # one f64 joint-mass word per reachable node
     achieved_gbs = alg_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
@@ -271,12 +305,18 @@ def main():
             "single_solve": single,
             "roofline": {"bound": "fp64-valu", "achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": fp64_tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kname,
-                         "flop_per_node": flop_node, "reach_nodes_per_date": plan.reach_nodes,
+                         "flop_per_node": flop_node,
+                         "flop_basis": "nodes evaluated (device count)" if nodes_eval is not None
+                                       else "reachable nodes",
+                         "nodes_evaluated_per_date": (nodes_eval / per) if nodes_eval is not None else None,
+                         "reach_nodes_per_date": plan.reach_nodes,
                          "dates_per_launch": per, "flop_per_launch": flop_launch,
                          "avg_launch_us": dom_avg_s * 1e6, "launches": dom_n,
-                         "timing": "HIP events on the kernel's stream, a separate one-batch leg (one launch in "
-                                   "flight); the timed legs carry no events",
+                         "timing": timing_note,
                          "event_leg_ms_per_step": el_r / a.steps * 1e3,
+                         "reach_basis": {"flop_per_launch": flop_reach,
+                                         "frac": flop_reach / dom_avg_s / 1e12 / FP64_PEAK_TFLOPS
+                                         if dom_avg_s > 0 else 0.0},
                          "hbm": {"alg_bytes_per_launch": alg_bytes, "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                                  "pmc_bytes_per_launch": traffic}},

@@ -167,6 +167,17 @@ class QuadraturePlan:
                 "cvq_plan_kernel_time")
         return float(ms.value), int(n.value)
 
+    def count_nodes(self, on: bool = True) -> None:
+        """Record, in the following solves, how many quadrature nodes each date evaluates
+        (COMPACT / SORTED / SWEEP; measurement aid, slower -- never in a timed run)."""
+        N.check(N.lib().cvq_plan_count_nodes(self._h, 1 if on else 0), "cvq_plan_count_nodes")
+
+    def nodes_evaluated(self) -> int:
+        """Nodes evaluated by the last counted solve, summed over its dates."""
+        n = C.c_int64()
+        N.check(N.lib().cvq_plan_nodes_evaluated(self._h, C.byref(n)), "cvq_plan_nodes_evaluated")
+        return int(n.value)
+
     # ------------------------------------------------------------ per-date inputs
     def set_dates(self, integrations_params_t) -> None:
         """integrations_params_t as the reference builds it: MSM (forecasts_by_states

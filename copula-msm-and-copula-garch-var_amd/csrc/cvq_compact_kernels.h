@@ -470,6 +470,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     auto stamp = [&](int idx) {                     // diagnostic only (never in a timed run)
         if (stamps && tid == 0 && idx < 32) stamps[idx] = __builtin_amdgcn_s_memtime();
     };
+    // nodes this thread evaluated (stamps only: added to stamps[28] per date, zeroed by the host)
+    int nev = 0;
     // issue priority by phase (CVQ_COMPACT_PRIO): the SIMD arbiter favours older waves, so the
     // last date to arrive on a CU lags the others through every phase; a wave that is further
     // along lowers its priority so the dates sharing a CU keep pace with each other
@@ -524,18 +526,21 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if constexpr (MSM) {
             wr = wc = 0.0;
             if (q <= kQUnroll) {                                   // every load issued before the chains
-                double fr[kQUnroll], fc[kQUnroll];
+                double fr[kQUnroll], fc[kQUnroll], wa[kQUnroll], wb[kQUnroll];
 #pragma unroll
                 for (int b = 0; b < kQUnroll; ++b) {
                     const int bb = min(b, q - 1);
+                    wa[b] = fb[bb];
+                    wb[b] = fb[q + bb];
                     fr[b] = S.F[(size_t)bb * n + i];
                     fc[b] = S.F[((size_t)q + bb) * n + i];
                 }
+                // states b >= q: weight 0 (F finite: fma(0, F, w) == w), so no load waits
+                // behind a branch on b < q
 #pragma unroll
                 for (int b = 0; b < kQUnroll; ++b) {
-                    const int bb = min(b, q - 1);
-                    wr = b < q ? fma(fb[bb], fr[b], wr) : wr;
-                    wc = b < q ? fma(fb[q + bb], fc[b], wc) : wc;
+                    wr = fma(b < q ? wa[b] : 0.0, fr[b], wr);
+                    wc = fma(b < q ? wb[b] : 0.0, fc[b], wc);
                 }
             } else {
                 for (int b = 0; b < q; ++b) {
@@ -639,6 +644,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         for (int k = 0; k < RPT; ++k) {
             const int len = own[k] ? max(kb[k] - ka[k], 0) : 0;
             if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
+            nev += len;
             ns += len;
             nb += own[k] ? max(bhi[k] - blo[k], 0) : 0;
         }
@@ -671,6 +677,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             const int m1 = a1 + (b1 - a1 + 1) / 2, m2 = a2 + (b2 - a2 + 1) / 2;
             if (m1 > a1) part += range_sum(r1, a1 + 1, m1);
             if (b2 > m2) part += range_sum(r2, m2 + 1, b2);
+            nev += max(m1 - a1, 0) + max(b2 - m2, 0);
         }
         sums[0] = team_sum1<NT>(part, red, parity);
     };
@@ -747,6 +754,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             for (int k = 0; k < RPT; ++k) {
                 const int len = own[k] ? max(kb[k] - ka[k], 0) : 0;
                 if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
+                nev += len;
             }
             val = team_sum1<NT>(part, red, parity);
         } else {
@@ -797,6 +805,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         for (int m = 0; m < NPT; ++m) wd[m] = (tid * NPT + m < cnt) ? tl[tid * NPT + m] : 0u;
         double pre[NPT];                                          // local inclusive prefix
         double run = 0.0;
+        nev += min(max(cnt - tid * NPT, 0), NPT);
 #pragma unroll
         for (int m = 0; m < NPT; ++m) {
             const int r = (int)(wd[m] & kTlRowMask), j = (int)((wd[m] >> kTlColShift) & kTlRowMask);
@@ -902,8 +911,10 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             if (!own[k]) continue;
-            for (int j = kLo[k] + 1; j <= kHi[k] && off < kTailCap; ++j, ++off)   // total <= kTailCap
+            for (int j = kLo[k] + 1; j <= kHi[k] && off < kTailCap; ++j, ++off) {  // total <= kTailCap
                 tail[off] = make_double2(G.vstar[(size_t)row[k] * n + j], range_sum(row[k], j, j));
+                ++nev;
+            }
         }
         __syncthreads();
         stamp(29);
@@ -943,6 +954,10 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     }
     stamp(31);
     if (stamps && tid == 0) stamps[26] = __builtin_amdgcn_s_memrealtime();
+    if (stamps) {
+        const int w = (int)wave_sum((double)nev);                  // exact in a double
+        if (lane == 0 && w) atomicAdd(&stamps[28], (unsigned long long)w);
+    }
 
     if (tid == leader) {
         sn[P.K] = (lo + hi) / 2;

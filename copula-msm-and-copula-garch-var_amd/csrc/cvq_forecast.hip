@@ -440,7 +440,7 @@ __global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const dou
                                                         long long N, long long n_in, long long T,
                                                         double* __restrict__ Pre, long long pstride,
                                                         double* __restrict__ Suf1, long long ustride,
-                                                        double* __restrict__ Gf, long long gstride, int* err) {
+                                                        double* __restrict__ Gf, long long gstride, int* flags) {
     constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
     __shared__ double cl[kScanB * S];                           // c_i[s] of the block's steps
     __shared__ double cm[kScanB];                               // 1 / max_s c_i
@@ -450,8 +450,19 @@ __global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const dou
     const long long b0 = (long long)blockIdx.x * kScanB;
     const long long b1 = min(b0 + kScanB, N);                    // steps [b0, b1)
     const int nb = (int)(b1 - b0);
-    for (int k = threadIdx.x; k < nb * S; k += blockDim.x)
-        cl[k] = cond_prob(r[b0 + k / S], P.vs[k % S]);
+    {
+        // entry k = tid + 4 S m is step tid / S + 4 m, state tid % S: every return of the block
+        // loaded before the first density (one memory latency instead of kScanB / 4)
+        constexpr int PER = kScanB / 4;
+        const int s = threadIdx.x % S, o0 = threadIdx.x / S;
+        double rv[PER];
+#pragma unroll
+        for (int m = 0; m < PER; ++m) rv[m] = (o0 + 4 * m < nb) ? r[b0 + o0 + 4 * m] : 0.0;
+        const double vs = P.vs[s];
+#pragma unroll
+        for (int m = 0; m < PER; ++m)
+            if (o0 + 4 * m < nb) cl[(o0 + 4 * m) * S + s] = cond_prob(rv[m], vs);
+    }
     __syncthreads();
     bool bad = false;
     for (int o = threadIdx.x; o < nb; o += blockDim.x) {
@@ -460,7 +471,9 @@ __global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const dou
         bad |= !(m > 0.0);                                       // every state's density is 0: calc_prob.py:64-65
         cm[o] = 1.0 / m;
     }
-    __syncthreads();
+    // this block's error flag, overwritten by every run (no reset launch between runs)
+    const int badb = __syncthreads_or(bad);
+    if (blockIdx.z == 0 && threadIdx.x == 0) flags[blockIdx.y * gridDim.x + blockIdx.x] = badb ? 1 : 0;
     double v[SL];
 #pragma unroll
     for (int j = 0; j < SL; ++j) v[j] = (lane_q * SL + j == q) ? 1.0 : 0.0;
@@ -483,7 +496,6 @@ __global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const dou
                 for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
             }
         }
-        if (bad) atomicOr(err, 1);
     } else {                                                     // Suf: rows, backward
         double* suf = Suf1 + blockIdx.y * ustride;
         for (int o = nb - 1; o >= 0; --o) {
@@ -521,10 +533,23 @@ __global__ __launch_bounds__(4 << K) void k_msm_supscan(const double* __restrict
     const long long s1 = min(s0 + kScanC, nfull);
     Gf += blockIdx.y * gstride;
     {
+        // the superblock's block products (kScanC S^2 doubles, 2 S double2 per thread): every
+        // load issued before the first LDS store (one memory latency instead of 2 S in a row)
+        constexpr int PER = kScanC * S * S / 2 / (4 * S);
         const double2* src = (const double2*)(Gf + s0 * S * S);
         double2* dst = (double2*)gl;
         const int nv = (int)((s1 - s0) * S * S / 2);
-        for (int k = threadIdx.x; k < nv; k += blockDim.x) dst[k] = src[k];
+        double2 tmp[PER];
+#pragma unroll
+        for (int m = 0; m < PER; ++m) {
+            const int k = threadIdx.x + m * 4 * S;
+            tmp[m] = k < nv ? src[k] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int m = 0; m < PER; ++m) {
+            const int k = threadIdx.x + m * 4 * S;
+            if (k < nv) dst[k] = tmp[m];
+        }
     }
     __syncthreads();
     double v[SL];
@@ -640,30 +665,27 @@ __global__ __launch_bounds__(256) void k_msm_scanwin(const double* __restrict__ 
                 return SG + ((sa + k) * kScanC) * S * S;      // full superblock sa + k
         }
     };
-    double x[S];
+    // the first kPre factors' rows and Suf_{b0}(t) u are loaded together (one memory latency;
+    // n_in = 1135 windows take 3-4 factors), later factors one ahead of their use
+    constexpr int kPre = 4;
+    double x[S], fm[kPre][S];
+#pragma unroll
+    for (int c = 0; c < S; ++c) x[c] = Suf1[tt * S + c];         // Suf_{b0}(t) u, up to a factor
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+        const double* m = mat(k < cnt ? k : 0) + row * S;
+#pragma unroll
+        for (int c = 0; c < S; ++c) fm[k][c] = m[c];
+    }
     {
         double tot = 0.0;
 #pragma unroll
-        for (int c = 0; c < S; ++c) {
-            x[c] = Suf1[tt * S + c];                             // Suf_{b0}(t) u, up to a factor
-            tot += x[c];
-        }
+        for (int c = 0; c < S; ++c) tot += x[c];
         const double inv = 1.0 / tot;
 #pragma unroll
         for (int c = 0; c < S; ++c) x[c] *= inv;
     }
-    double cur[S], nxt[S];
-    {
-        const double* m0 = mat(0) + row * S;
-#pragma unroll
-        for (int c = 0; c < S; ++c) cur[c] = m0[c];
-    }
-    for (long long k = 0; k < cnt; ++k) {
-        if (k + 1 < cnt) {
-            const double* m1 = mat(k + 1) + row * S;
-#pragma unroll
-            for (int c = 0; c < S; ++c) nxt[c] = m1[c];
-        }
+    auto apply = [&](const double (&cur)[S]) {                   // x <- normalise(F x)
         double y = 0.0;
 #pragma unroll
         for (int c = 0; c < S; ++c) y = fma(cur[c], x[c], y);
@@ -675,9 +697,27 @@ __global__ __launch_bounds__(256) void k_msm_scanwin(const double* __restrict__ 
         }
         const double inv = 1.0 / tot;
 #pragma unroll
-        for (int c = 0; c < S; ++c) {
-            x[c] *= inv;
-            cur[c] = nxt[c];
+        for (int c = 0; c < S; ++c) x[c] *= inv;
+    };
+#pragma unroll
+    for (int k = 0; k < kPre; ++k)
+        if (k < cnt) apply(fm[k]);
+    if (cnt > kPre) {
+        double cur[S], nxt[S];
+        {
+            const double* m0 = mat(kPre) + row * S;
+#pragma unroll
+            for (int c = 0; c < S; ++c) cur[c] = m0[c];
+        }
+        for (long long k = kPre; k < cnt; ++k) {
+            if (k + 1 < cnt) {
+                const double* m1 = mat(k + 1) + row * S;
+#pragma unroll
+                for (int c = 0; c < S; ++c) nxt[c] = m1[c];
+            }
+            apply(cur);
+#pragma unroll
+            for (int c = 0; c < S; ++c) cur[c] = nxt[c];
         }
     }
     if (!active || g >= M.q) return;
@@ -1212,6 +1252,14 @@ ScanLayout scan_layout(int k, long long n_in, long long T) {
     return L;
 }
 
+// error flags of the scan filter: one per (asset, block) of k_msm_blkscan, after the error
+// word's two doubles (0 when the scan filter does not run)
+long long scan_flag_count(int k, long long n_in, long long T, int dim) {
+    if (!msm_scan_ok(k, n_in)) return 0;
+    const long long N = n_in + T - 1;
+    return dim * ((N + kScanB - 1) / kScanB);
+}
+
 template <int K>
 void launch_scan(const MsmParamsN& P, const StateMapQ& MQ, int dim, const double* r, long long N, long long n_in,
                  long long T, double* buf, double* fbs, int* err, hipStream_t stream) {
@@ -1274,7 +1322,8 @@ int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, 
         const int B = msm_block_len(k, n_in);
         G = B ? dim * (N / B) * S * S : 0;                  // blocked filter: full-block products
     }
-    *doubles = dim * N * S + dim * T * S + G + 2;          // cond, filtered probabilities, [G], error word
+    // cond, filtered probabilities, [G], error word (2 doubles), scan filter: per-block error flags
+    *doubles = dim * N * S + dim * T * S + G + 2 + (scan_flag_count(k, n_in, T, dim) + 1) / 2;
     return CVQ_OK;
 }
 
@@ -1312,13 +1361,15 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
         gsz = dim * (L.pre + L.suf + L.gf + 2 * L.sup);
     }
     int* err = (int*)(G + gsz);
-    CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
+    // the scan filter's blocks overwrite their own error flags (err + 4 ...) on every run; the
+    // step-by-step and blocked filters OR into the error word, reset here
+    if (!scan) CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
     if (scan) {                        // densities computed per block inside; the collapse fused into the windows
         StateMapQ MQ{};
         MQ.q = q;
         for (int d = 0; d < dim; ++d)
             for (int s2 = 0; s2 < S; ++s2) MQ.u[d][s2] = M.u[d][s2];
-        rc = launch_scan_k(k, P, MQ, dim, returns_c, N, n_in, T, G, fbs_out, err, st);
+        rc = launch_scan_k(k, P, MQ, dim, returns_c, N, n_in, T, G, fbs_out, err + 4, st);
         if (rc) return rc;
     } else {
         hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,
@@ -1347,9 +1398,17 @@ int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n
         G = B ? dim * (N / B) * S * S : 0;
     }
     int e = 0;
-    CVQ_HIP_CHECK(hipMemcpyAsync(&e, scratch + dim * N * S + dim * T * S + G, sizeof(int), hipMemcpyDeviceToHost,
-                                 (hipStream_t)stream));
-    CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    const int* err = (const int*)(scratch + dim * N * S + dim * T * S + G);
+    if (msm_scan_ok(k, n_in)) {                            // the last run's per-block flags
+        std::vector<int> fl((size_t)scan_flag_count(k, n_in, T, dim));
+        CVQ_HIP_CHECK(hipMemcpyAsync(fl.data(), err + 4, fl.size() * sizeof(int), hipMemcpyDeviceToHost,
+                                     (hipStream_t)stream));
+        CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+        for (int f : fl) e |= f;
+    } else {
+        CVQ_HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+        CVQ_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    }
     CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");
     return CVQ_OK;
 }

@@ -146,6 +146,8 @@ struct cvq_plan {
     long long capIO = 0;
     double* d_io = nullptr;      // bounds (2T) + out (T) / var (T)
     unsigned long long* d_stamps = nullptr;   // diagnostic phase stamps (CVQ_STAMPS=1)
+    bool count_nodes = false;    // cvq_plan_count_nodes: solves record their node counts (stamps)
+    bool nodes_valid = false;    // the last solve recorded them
     // COMPACT: host grid copy, v* table, grid lookup buckets, fixed-level cuts for the
     // cached solve arguments
     std::vector<double> hx;
@@ -352,6 +354,8 @@ int ensure_stamps(cvq_plan* p) {
         CVQ_HIP_CHECK(hipMalloc((void**)&p->d_stamps, (size_t)p->T * 32 * 8));
         p->capStamps = p->T;
     }
+    // slot 28 of each date accumulates its node count (COMPACT adds per wave)
+    CVQ_HIP_CHECK(hipMemsetAsync(p->d_stamps, 0, (size_t)p->T * 32 * 8, p->stream));
     return CVQ_OK;
 }
 
@@ -828,8 +832,10 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     if (sorted_family(p)) {
         int rc = ensure_sorted_tree(p, P);
         if (rc) return rc;
-        static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;   // diagnostic phase stamps
+        static const bool env_stamps = getenv("CVQ_STAMPS") != nullptr;   // diagnostic phase stamps
+        const bool dbg_stamps = env_stamps || p->count_nodes;
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
+        p->nodes_valid = p->count_nodes;
         return launch_sorted(p->S, P, sorted_geom(p, true), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
                              direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
                              dbg_stamps ? (double*)p->d_stamps : nullptr,
@@ -838,10 +844,12 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
         if (rc) return rc;
-        static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
+        static const bool env_stamps = getenv("CVQ_STAMPS") != nullptr;
+        const bool dbg_stamps = env_stamps || p->count_nodes;
         double* st = nullptr;
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         if (dbg_stamps) st = (double*)p->d_stamps;
+        p->nodes_valid = p->count_nodes;
         if (p->capDefer < p->T + 2) {                      // zeroed once; the generic kernel resets it
             if ((rc = dev_alloc(&p->d_defer, (size_t)p->T + 2))) return rc;
             CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
@@ -1354,6 +1362,29 @@ int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
     CVQ_REQUIRE(count <= p->capStamps * 32, CVQ_ERR_INVALID, "count exceeds the stamp buffer");
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     CVQ_HIP_CHECK(hipMemcpy(host, p->d_stamps, count * 8, hipMemcpyDeviceToHost));
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_count_nodes(cvq_plan* p, int32_t enable) {
+    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
+    CVQ_REQUIRE(!enable || p->strategy == CVQ_STRATEGY_COMPACT || p->strategy == CVQ_STRATEGY_SORTED ||
+                    p->strategy == CVQ_STRATEGY_SWEEP,
+                CVQ_ERR_UNSUPPORTED, "node counts are recorded by the COMPACT, SORTED and SWEEP solves");
+    p->count_nodes = enable != 0;
+    p->nodes_valid = false;
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_nodes_evaluated(cvq_plan* p, int64_t* total) {
+    CVQ_REQUIRE(p != nullptr && total != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(p->nodes_valid && p->d_stamps != nullptr, CVQ_ERR_STATE,
+                "no node counts recorded (cvq_plan_count_nodes(plan, 1), then cvq_solve)");
+    std::vector<unsigned long long> h((size_t)p->T * 32);
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    CVQ_HIP_CHECK(hipMemcpy(h.data(), p->d_stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    long long s = 0;
+    for (long long t = 0; t < p->T; ++t) s += (long long)h[(size_t)t * 32 + 28];
+    *total = s;
     return CVQ_OK;
 }
 

@@ -85,12 +85,17 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
         const double* ph = S.phi + (size_t)d * S.q * S.n + i;
         double acc;
         if (S.q <= kQUnroll) {                                   // every load issued before the sum
-            double pv[kQUnroll];
+            // the weights of states s >= q are 0 (their Phi loads repeat state q - 1's finite
+            // values), so acc + 0 * pv[s] leaves the sum bit for bit unchanged and no scalar
+            // load waits behind a branch on s < q
+            double pv[kQUnroll], fv[kQUnroll];
+#pragma unroll
+            for (int s = 0; s < kQUnroll; ++s) fv[s] = f[min(s, S.q - 1)];
 #pragma unroll
             for (int s = 0; s < kQUnroll; ++s) pv[s] = ph[(size_t)min(s, S.q - 1) * S.n];
-            acc = f[0] * pv[0];
+            acc = fv[0] * pv[0];
 #pragma unroll
-            for (int s = 1; s < kQUnroll; ++s) acc = s < S.q ? acc + f[min(s, S.q - 1)] * pv[s] : acc;
+            for (int s = 1; s < kQUnroll; ++s) acc = acc + (s < S.q ? fv[s] : 0.0) * pv[s];
         } else {
             acc = f[0] * ph[0];
             for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];

@@ -118,6 +118,12 @@ int32_t cvq_plan_kernel_time(cvq_plan* plan, int32_t kind, double* total_ms, int
  * solve, recorded only when the process runs with CVQ_STAMPS=1 (never in a timed
  * run).  host receives count uint64 values, 32 per date. */
 int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
+/* Measurement aid (bench.py's FP64 roofline basis): with cvq_plan_count_nodes(plan, 1)
+ * the following COMPACT / SORTED / SWEEP solves record how many quadrature nodes each
+ * date evaluated (the phase-stamp buffer: slower, never in a timed run);
+ * cvq_plan_nodes_evaluated returns the last such solve's total over its dates. */
+int32_t cvq_plan_count_nodes(cvq_plan* plan, int32_t enable);
+int32_t cvq_plan_nodes_evaluated(cvq_plan* plan, int64_t* total);
 
 /* Per-date inputs = integrations_params_t (calc_integral.py:158):
  *   MSM:       a = forecasts_by_states [T][dim][q], b = forecasts [T][n_combos]
@@ -194,7 +200,8 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
  * returns_c (device) [dim][n_in + T - 1] centred returns; scratch (device) of
  * cvq_msm_tables_scratch doubles; fbs_out (device) [T][dim][q]; pi_out (device)
  * [T][q**dim].  cvq_msm_tables_status synchronises and reports a zero Bayes
- * normaliser (calc_prob.py:64-65) as CVQ_ERR_NUMERIC. */
+ * normaliser (calc_prob.py:64-65) of the last cvq_msm_tables run on that scratch as
+ * CVQ_ERR_NUMERIC. */
 int32_t cvq_msm_tables_scratch(int32_t dim, int32_t k, int64_t n_in, int64_t T, int64_t* doubles);
 int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, const double* params,
                        const int32_t* state_map, int32_t q, const double* returns_c, int64_t n_in,

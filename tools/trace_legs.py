@@ -1,14 +1,14 @@
 """Split a rocprofv3 kernel trace of one bench.py run into its legs (GPU-box tool).
 
 bench.py runs, in order: the in-flight leg (warmup + steps launches of the dominant
-kernel), the single-solve leg (warmup + steps, one batch at a time), the event-timed
-roofline leg (the same, with HIP events), then the e2e leg (warmup + steps).  The
-dominant kernel's dispatches, in start-time order, are cut accordingly and each leg's
-average kernel duration and launch-to-launch gap are printed -- the roofline leg's
-average is what bench.py's HIP events time for "roofline".
+kernel), the single-solve leg (warmup + steps, one batch at a time; two HIP events
+bracket its timed launches, and bracket / steps is bench.py's "roofline" launch time),
+one node-counting solve (1 launch), then the e2e leg (warmup + steps).  The dominant
+kernel's dispatches, in start-time order, are cut accordingly and each leg's average
+kernel duration and launch-to-launch gap are printed.
 
 usage: python tools/trace_legs.py <dir with *kernel_trace.csv> [--steps 100 --warmup 5 --kernel k_compact
-       --legs inflight,single_solve,roofline,e2e]
+       --legs inflight,single_solve,count=1,e2e]      (name=N: a leg of N launches, all timed)
 """
 import csv
 import glob
@@ -35,11 +35,15 @@ def main():
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
     per = warmup + steps
-    names = arg("--legs", "inflight,single_solve,roofline,e2e").split(",")
-    legs = [(nm, i * per) for i, nm in enumerate(names)]
+    legs, off = [], 0
+    for ent in arg("--legs", "inflight,single_solve,count=1,e2e").split(","):
+        nm, _, cnt = ent.partition("=")
+        n_l, w_l = (int(cnt), 0) if cnt else (per, warmup)
+        legs.append((nm, off + w_l, off + n_l))
+        off += n_l
     print(f"{len(rows)} dispatches of {kern} (fast instance); legs of {per} = {warmup} warmup + {steps} timed")
-    for nm, off in legs:
-        seg = rows[off + warmup: off + per]
+    for nm, lo, hi in legs:
+        seg = rows[lo: hi]
         if not seg:
             continue
         d = [(e - s) / 1e3 for s, e, _ in seg]
