@@ -23,6 +23,7 @@ struct StaticDev {
     int uni_m;                    // 2 * (nu+1)/2 when a half-integer <= 16, else -1
     double term1;                 // multivariate density constant (student.py:138 / gaussian.py:107)
     double g_uni;                 // univariate t constant (student.py:164)
+    double inv_g_uni;             // 1 / g_uni (the integer-nu table path multiplies)
     double inv_nu, nu, theta;
     double Ri[9];                 // inverse correlation, row-major dim x dim
     double w0, w1, w2;            // portfolio weights
@@ -67,7 +68,7 @@ struct alignas(16) Header {       // per-rank solve summary, all-gathered across
 // Layout key of the structs passed between translation units (cvq_plan.hip launches the
 // kernels compiled in cvq_compact.hip / cvq_sorted.hip): a stale object fails its launch
 // with CVQ_ERR_STATE instead of reading misplaced pointers.
-constexpr size_t kAbiVersion = 3;
+constexpr size_t kAbiVersion = 4;
 __host__ __device__ constexpr size_t kernel_abi_key() {
     return kAbiVersion * 1000003u + sizeof(StaticDev) * 4099u + sizeof(SolveConst) * 67u + sizeof(Header);
 }

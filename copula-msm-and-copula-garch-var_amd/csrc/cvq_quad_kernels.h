@@ -110,11 +110,24 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
     }
 }
 
-template <int COP, bool MSM, bool TAB = false>
+#ifndef CVQ_TABLE_INT_NU
+#define CVQ_TABLE_INT_NU 1
+#endif
+// NUI > 0 (with TAB): the Student nu is the integer NUI -- quantile tail variable by root_nu,
+// B = pdf (1 + z^2/nu)^((nu+1)/2) / g_uni without divisions (~1 ulp from the reference's
+// arithmetic; the VaR tolerates ~1e-8 relative node noise)
+template <int COP, bool MSM, bool TAB = false, int NUI = 0>
 __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __restrict__ a, long long td, int d,
                                             int i, double* A_out, double* B_out) {
     double u, pdf;
     marginal_u<MSM>(S, a, td, d, i, &u, &pdf);
+    if constexpr (COP == CVQ_STUDENT && TAB && NUI > 0 && CVQ_TABLE_INT_NU) {
+        const double z = stdtrit_tab_int<NUI>(S.tk, u);                              // student.py:102
+        const double pw = pow_half_pos(fma(z * z, S.inv_nu, 1.0), S.uni_m, -S.uni_ex);   // :164-172
+        *A_out = z;
+        *B_out = isfinite(z) ? (pdf * pw) * S.inv_g_uni : pdf * pos_inf();
+        return;
+    }
     if (COP == CVQ_PLACKETT) {
         *A_out = u;
         *B_out = pdf;

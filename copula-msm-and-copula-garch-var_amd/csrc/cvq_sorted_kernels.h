@@ -320,7 +320,8 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         for (int ax = 0; ax < DIM; ++ax) {
             double A, B;
             if constexpr (FUSED) {
-                table_entry<COP, MSM, COP == CVQ_STUDENT>(S, a, t * DIM + ax, ax, i, &A, &B);
+                table_entry<COP, MSM, COP == CVQ_STUDENT, (COP == CVQ_STUDENT && PM == 6 + DIM) ? 6 : 0>(
+                    S, a, t * DIM + ax, ax, i, &A, &B);
             } else {
                 A = tA[(t * DIM + ax) * n + i];
                 B = tB[(t * DIM + ax) * n + i];

@@ -37,6 +37,16 @@ if STRAT == "compact" and (st[:, 27] != 0).any():
     dur = (st[:, 26] - st[:, 25]).astype(np.float64)
     print(f"placement: {uk.size} distinct CUs for {T} workgroups; per-CU count histogram "
           f"{dict(zip(*np.unique(cnt, return_counts=True)))}; XCDs {np.unique(xcc).size}")
+    if (st[:, 20] != 0).any():
+        # SIMD of each wave (HW_ID bits 5:4): are the waves that carry a date's long rows on
+        # the same SIMD for every date of a CU?
+        simd = (st[:, 20:24] >> 4) & 3
+        for w in range(4):
+            print(f"  wave {w}: SIMD histogram {np.bincount(simd[:, w], minlength=4).tolist()}")
+        same = [np.unique(simd[inv == k, 0]).size == 1 for k in range(uk.size) if (inv == k).sum() > 1]
+        print(f"  CUs whose dates' wave 0 all share one SIMD: {sum(same)} of {len(same)}")
+        print(f"  wave SIMD = (wave + c) mod 4 for every date: "
+              f"{bool(((simd - simd[:, :1]) % 4 == np.arange(4)).all())}")
     per_wg = cnt[inv]
     for c in np.unique(per_wg):
         m = per_wg == c
