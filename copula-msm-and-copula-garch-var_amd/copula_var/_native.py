@@ -153,8 +153,9 @@ def ptr(a: np.ndarray) -> C.c_void_p:
 
 
 def special(fn: str, x, nu: float = 0.0, device: int = 0) -> np.ndarray:
-    """Device t.ppf / norm.ppf / erf (known-answer tests)."""
-    code = {"tppf": 0, "ndtri": 1, "erf": 2}[fn]
+    """Device t.ppf / norm.ppf / erf (known-answer tests); "tppf6": the solve kernels'
+    integer-nu t.ppf (nu = 6)."""
+    code = {"tppf": 0, "ndtri": 1, "erf": 2, "tppf6": 3}[fn]
     xx = f64(x).ravel()
     out = np.empty_like(xx)
     check(lib().cvq_special(device, code, float(nu), ptr(xx), xx.size, ptr(out), MEM_HOST), f"cvq_special({fn})")

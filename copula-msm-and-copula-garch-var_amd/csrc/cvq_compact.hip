@@ -9,7 +9,6 @@ namespace cvq {
 
 int compact_max_n() { return 8 * CVQ_COMPACT_NT; }
 int compact_tail_cap() { return CVQ_COMPACT_NT * kBlkPerThread; }   // block tail: cell nodes per workgroup
-int compact_nt() { return CVQ_COMPACT_NT; }                          // threads per date (fixed-slab segments)
 
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,

@@ -103,22 +103,7 @@ constexpr int kNoPos = 0x7FFFFFFF;                  // "no such position" in the
 #ifndef CVQ_COMPACT_PRIO
 #define CVQ_COMPACT_PRIO 0
 #endif
-// A/B switches (r03): CVQ_ROW_ROT = 1 rotates the row <-> thread map by a multiple of 64 per
-// date, so the waves that carry a slab's long rows (the bisection levels' rows x_r < 0, the
-// (lower, fg] triangle's rows) land on different SIMDs for the dates sharing a CU;
-// CVQ_WALK_PRIO = 1 raises the leader wave's issue priority for the block tail's serial walk
-#ifndef CVQ_ROW_ROT
-#define CVQ_ROW_ROT 0
-#endif
-#ifndef CVQ_WALK_PRIO
-#define CVQ_WALK_PRIO 0
-#endif
-// CVQ_LEVEL_PAIR = 1: a bisection level's slab in row r is summed half by row r's owner and
-// half by the owner of row n - 1 - r (the fixed slabs' long-with-short pairing), so the
-// levels' rows (x_r < 2v + 5: the lower rows for v < 0) spread over every wave of the date
-#ifndef CVQ_LEVEL_PAIR
-#define CVQ_LEVEL_PAIR 0
-#endif
+
 template <int P>
 __device__ __forceinline__ void phase_prio() {
     if constexpr (CVQ_COMPACT_PRIO != 0) __builtin_amdgcn_s_setprio(P);
@@ -142,12 +127,7 @@ struct CompactGeom {
     const uint32_t* tlist;
     const double* tvs;
     int bstart[4];
-    // fixed slabs (lower, fg], (sg0, fg], (fg, sg1] as at most kFsegPer row segments per thread
-    // ([3][NT][kFsegPer] words: row | j0 << 11 | len << 22, nodes j0 + 1 .. j0 + len), host-balanced;
-    // nullptr: the long-with-short row pairing
-    const uint32_t* fseg;
 };
-constexpr int kFsegPer = 3;
 
 // ------------------------------------------------------------------ reductions
 template <int CTRL, int ROWMASK = 0xF>
@@ -521,11 +501,9 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         stamps[20 + (tid >> 6)] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     int row[RPT];
     bool own[RPT];
-    // rows owned by this thread: tid + NT k, or (CVQ_ROW_ROT) rotated by 64 rot per date
-    const int rot = CVQ_ROW_ROT ? 64 * (int)((t + (t >> 8)) & 3) : 0;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-        row[k] = ((tid + rot) & (NT - 1)) + NT * k;
+        row[k] = tid + NT * k;
         own[k] = row[k] < n;
     }
     // static LDS images (grid, lookup buckets, fixed-level cuts): every load issued here,
@@ -535,13 +513,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     constexpr int kBkPer = kBucketsPerPoint * RPT, kCutPer = (kCutLds / 2) * RPT;
     double xv[RPT];
     int bv[kBkPer], cv[kCutPer];
-    // the fixed slabs' row segments of this thread (host-balanced table): loaded up front
-    const bool fsg = G.fseg != nullptr;
-    uint32_t fw[3][kFsegPer];
-#pragma unroll
-    for (int sl = 0; sl < 3; ++sl)
-#pragma unroll
-        for (int m = 0; m < kFsegPer; ++m) fw[sl][m] = fsg ? G.fseg[((size_t)sl * NT + tid) * kFsegPer + m] : 0u;
+
 #pragma unroll
     for (int k = 0; k < RPT; ++k) xv[k] = S.x[min(tid + NT * k, n - 1)];
 #pragma unroll
@@ -680,6 +652,15 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             for (int u = 0; u + h < IL; u += 2 * h) acc[u] += acc[u + h];
         return fr.scale * acc[0];
     };
+    // one node (r, j) (the block tail): range_sum(r, j, j) without its loops, same arithmetic
+    auto node1 = [&](int rr, int j) -> double {
+        if constexpr (GEN) {
+            if (!fast) return generic_node<COP, MSM>(S, rowr + RR * rr, col[kColRec * j], colg + cgs * j, rr, j, rank1, pit);
+        }
+        const FastRow fr = load_fast_row<COP, SI>(rowr + RR * rr);
+        const double2 cz = *(const double2*)(col + kColRec * j);
+        return fr.scale * fma(fast_f<COP, PM>(S, fr, cz.x), cz.y, 0.0);
+    };
     // one level's workgroup sums: slab (ka, kb] sum, its node count, bracket (blo, bhi] nodes
     double sums[3];
     auto level_sums = [&](const int (&ka)[RPT], const int (&kb)[RPT], const int (&blo)[RPT], const int (&bhi)[RPT]) {
@@ -727,38 +708,14 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         sums[0] = team_sum1<NT>(part, red, parity);
     };
 
-    // fixed slab from the host's balanced segments: <= kFsegPer row ranges per thread
-    auto seg_slab = [&](const uint32_t (&w)[kFsegPer]) {
-        double part = 0.0;
-#pragma unroll
-        for (int m = 0; m < kFsegPer; ++m) {
-            const int len = (int)(w[m] >> 22);
-            if (len > 0) {
-                const int r = (int)(w[m] & 0x7FFu), j0 = (int)((w[m] >> 11) & 0x7FFu);
-                part += range_sum(r, j0 + 1, j0 + len);
-                nev += len;
-            }
-        }
-        sums[0] = team_sum1<NT>(part, red, parity);
-    };
-
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    if (fsg) seg_slab(fw[0]);
-    else fixed_slab(P.lower, P.fg);
+    fixed_slab(P.lower, P.fg);
     const double r0 = sums[0];
     stamp(2);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    if (fsg) {
-        // (sg0, fg] (slab 1), (fg, sg1] (slab 2), or empty (NaN r0: nl = nu = fg)
-        uint32_t w2[kFsegPer];
-#pragma unroll
-        for (int m = 0; m < kFsegPer; ++m) w2[m] = nl == P.sg0 ? fw[1][m] : (nu == P.sg1 ? fw[2][m] : 0u);
-        seg_slab(w2);
-    } else {
-        fixed_slab(nl, nu);
-    }
+    fixed_slab(nl, nu);
     const double nr = sums[0];
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);
@@ -774,28 +731,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     for (int k = 0; k < RPT; ++k) {                              // NaN bracket (Q3): empty
         kLo[k] = (own[k] && lo == lo) ? fixcut(k, lo) : 0;
         kHi[k] = (own[k] && lo == lo) ? max((int)fixcut(k, hi), kLo[k]) : 0;
-    }
-    // CVQ_LEVEL_PAIR: the partner rows n - 1 - row[k] (second halves of their level slabs)
-    constexpr bool PAIR = CVQ_LEVEL_PAIR != 0;
-    double lev2[RPT];
-    int kLo2[RPT], kHi2[RPT], prow[RPT];
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        prow[k] = own[k] ? n - 1 - row[k] : 0;
-        lev2[k] = PAIR ? sx[prow[k]] * S.w1 : 0.0;
-        int a2 = 0, b2 = 0;
-        if (PAIR && own[k] && lo == lo) {
-            const int16_t* c = cfx + (size_t)prow[k] * kCutLds;
-            auto cut2 = [&](double v) {
-                return v == P.lower ? (int)c[kCutLower] : v == P.sg0 ? (int)c[kCutSg0] : v == P.fg ? (int)c[kCutFg]
-                     : v == P.sg1 ? (int)c[kCutSg1] : v == P.vmin ? (int)c[kCutVmin] : v == P.vmax ? (int)c[kCutVmax]
-                     : grid_count(sx, bk, G, inner_coord(S, v, lev2[k]), 0, n - 1);
-            };
-            a2 = cut2(lo);
-            b2 = max(cut2(hi), a2);
-        }
-        kLo2[k] = a2;
-        kHi2[k] = b2;
     }
     stamp(4);
     phase_prio<1>();
@@ -837,10 +772,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             ka[k] = ustack ? kLo[k] : kM[k];
             kb[k] = ustack ? kM[k] : kHi[k];
         }
-        int kM2[RPT];
-#pragma unroll
-        for (int k = 0; k < RPT; ++k)
-            kM2[k] = (PAIR && tabc && own[k]) ? grid_count(sx, bk, G, inner_coord(S, mid, lev2[k]), kLo2[k], kHi2[k]) : 0;
+
         double val;
         int Nlow = 0, Nbr = 0;
         if (tabc) {
@@ -848,18 +780,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
                 const int len = own[k] ? max(kb[k] - ka[k], 0) : 0;
-                if constexpr (PAIR) {
-                    // own row: first ceil(len / 2) columns; partner row: the rest of its slab
-                    const int h1 = (len + 1) >> 1;
-                    if (h1 > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + h1);
-                    const int a2 = ustack ? kLo2[k] : kM2[k], b2 = ustack ? kM2[k] : kHi2[k];
-                    const int len2 = own[k] ? max(b2 - a2, 0) : 0, h2 = (len2 + 1) >> 1;
-                    if (len2 > h2) part += range_sum(prow[k], a2 + h2 + 1, b2);
-                    nev += h1 + max(len2 - h2, 0);
-                } else {
-                    if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
-                    nev += len;
-                }
+                if (len > 0) part += range_sum(row[k], ka[k] + 1, ka[k] + len);
+                nev += len;
             }
             val = team_sum1<NT>(part, red, parity);
         } else {
@@ -879,19 +801,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             ps += tabc ? c_lo : 0;
             hc = 2 * hc + 1;
 #pragma unroll
-            for (int k = 0; k < RPT; ++k) {
-                kLo[k] = kM[k];
-                kLo2[k] = kM2[k];
-            }
+            for (int k = 0; k < RPT; ++k) kLo[k] = kM[k];
         } else {
             hi = mid;
             nbr_next = tabc ? c_lo : Nlow;
             hc = 2 * hc;
 #pragma unroll
-            for (int k = 0; k < RPT; ++k) {
-                kHi[k] = kM[k];
-                kHi2[k] = kM2[k];
-            }
+            for (int k = 0; k < RPT; ++k) kHi[k] = kM[k];
         }
         prev = Fn;
         prevU = mid;
@@ -920,7 +836,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
 #pragma unroll
         for (int m = 0; m < NPT; ++m) {
             const int r = (int)(wd[m] & kTlRowMask), j = (int)((wd[m] >> kTlColShift) & kTlRowMask);
-            const double v = (tid * NPT + m < cnt) ? range_sum(r, j, j) : 0.0;
+            const double v = (tid * NPT + m < cnt) ? node1(r, j) : 0.0;
             run += v;
             pre[m] = run;
         }
@@ -974,7 +890,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         __syncthreads();
         stamp(29);
         if (tid == leader) {
-            if constexpr (CVQ_WALK_PRIO != 0) __builtin_amdgcn_s_setprio(3);
             int ec = kNoPos, ez = kNoPos;
             uint32_t nc = 0u, nz_ = 0u;
 #pragma unroll

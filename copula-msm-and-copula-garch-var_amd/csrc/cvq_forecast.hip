@@ -1127,7 +1127,7 @@ __global__ void k_special(int fn, TConst tk, const double* __restrict__ x, long 
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double v = x[i];
-    out[i] = fn == 0 ? stdtrit(tk, v) : (fn == 1 ? ndtri(v) : erf(v));
+    out[i] = fn == 0 ? stdtrit(tk, v) : fn == 1 ? ndtri(v) : fn == 2 ? erf(v) : stdtrit_tab_int<6>(tk, v);
 }
 
 // ------------------------------------------------------------ host helpers
@@ -1691,14 +1691,17 @@ int32_t cvq_ukf_filter(int32_t device, const double* params, int64_t B, const do
 
 int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int64_t n, double* out, int32_t mem) {
     CVQ_REQUIRE(x && out && n >= 1, CVQ_ERR_INVALID, "bad argument");
-    CVQ_REQUIRE(fn >= 0 && fn <= 2, CVQ_ERR_INVALID, "fn must be 0 (t.ppf), 1 (norm.ppf) or 2 (erf)");
+    CVQ_REQUIRE(fn >= 0 && fn <= 3, CVQ_ERR_INVALID,
+                "fn must be 0 (t.ppf), 1 (norm.ppf), 2 (erf) or 3 (t.ppf, the solve kernels' nu = 6 path)");
+    CVQ_REQUIRE(fn != 3 || nu == 6.0, CVQ_ERR_INVALID, "fn 3 is the integer path for nu = 6");
     int rc = check_device(device);
     if (rc) return rc;
     TConst tk{};
     DevBuf cf;
-    if (fn == 0) {
+    if (fn == 0 || fn == 3) {
         CVQ_REQUIRE(nu > 0, CVQ_ERR_INVALID, "nu must be > 0");
         if ((rc = make_tconst(nu, &tk, &cf.p))) return rc;
+        CVQ_REQUIRE(fn != 3 || tk.q_c != nullptr, CVQ_ERR_UNSUPPORTED, "no direct t.ppf tables for this nu");
     }
     DevBuf xin, dout;
     const double* d_x;

@@ -108,7 +108,6 @@ int make_tconst(double nu, TConst* tk, double** d_cf) {
 }
 
 int compact_tail_cap();                      // cvq_compact.hip: the block tail's node capacity
-int compact_nt();                            // cvq_compact.hip: threads per date
 }  // namespace cvq
 
 using namespace cvq;
@@ -166,8 +165,6 @@ struct cvq_plan {
     double* d_tvs = nullptr;     // [n (n - 1)] = hvc on the device
     int bstart[4] = {0, 0, 0, 0};   // ub(bracket lower) in hvc for the cached solve arguments
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
-    uint32_t* d_fseg = nullptr;  // [3][NT][kFsegPer] balanced fixed-slab row segments (build_fixed_segments)
-    bool fseg_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
     // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
@@ -731,60 +728,6 @@ void build_cell_counts(const std::vector<double>& vs, const SolveConst& P, int c
 }
 
 // Fixed-level cut table (and the bisection cells' node counts) for the cached solve arguments.
-// Fixed slabs (lower, fg], (sg0, fg], (fg, sg1] of a COMPACT solve as <= kFsegPer row segments
-// per thread with equal node counts (date-independent: the cut table h).  The rows are ordered
-// longest, shortest, second longest, ... so a chunk of C consecutive nodes holds at most a long
-// row's tail, a short row and the next long row's head; C grows from ceil(nodes / NT) until every
-// chunk fits kFsegPer segments.  Returns false (pairing fallback) when a word cannot hold it.
-bool build_fixed_segments(const std::vector<int16_t>& h, int n, int NT, std::vector<uint32_t>& out) {
-    if (n > 2048) return false;
-    const int ca[3] = {kCutLower, kCutSg0, kCutFg}, cb[3] = {kCutFg, kCutFg, kCutSg1};
-    out.assign((size_t)3 * NT * kFsegPer, 0u);
-    struct Seg { int r, a, len; };
-    for (int sl = 0; sl < 3; ++sl) {
-        std::vector<Seg> rows;
-        long long total = 0;
-        for (int r = 0; r < n; ++r) {
-            const int a = h[(size_t)r * kCutFixed + ca[sl]];
-            const int b = std::max((int)h[(size_t)r * kCutFixed + cb[sl]], a);
-            if (b > a) rows.push_back({r, a, b - a});
-            total += std::max(b - a, 0);
-        }
-        if (total == 0) continue;
-        std::stable_sort(rows.begin(), rows.end(), [](const Seg& x, const Seg& y) { return x.len > y.len; });
-        std::vector<Seg> ord;
-        for (size_t i = 0, j = rows.size(); i < j;) {
-            ord.push_back(rows[i++]);
-            if (i < j) ord.push_back(rows[--j]);
-        }
-        const long long C0 = (total + NT - 1) / NT;
-        bool done = false;
-        for (long long C = C0; C <= 4 * C0 && C < 1024 && !done; ++C) {
-            std::vector<uint32_t> w((size_t)NT * kFsegPer, 0u);
-            int t = 0, nseg = 0;
-            long long used = 0;
-            bool ok = true;
-            for (const Seg& g : ord) {
-                for (int pos = 0; pos < g.len && ok;) {
-                    if (t >= NT || nseg == kFsegPer) { ok = false; break; }
-                    const int take = (int)std::min<long long>(g.len - pos, C - used);
-                    w[(size_t)t * kFsegPer + nseg++] = (uint32_t)g.r | ((uint32_t)(g.a + pos) << 11) | ((uint32_t)take << 22);
-                    used += take;
-                    pos += take;
-                    if (used == C) { ++t; used = 0; nseg = 0; }
-                }
-                if (!ok) break;
-            }
-            if (ok) {
-                std::copy(w.begin(), w.end(), out.begin() + (size_t)sl * NT * kFsegPer);
-                done = true;
-            }
-        }
-        if (!done) return false;
-    }
-    return true;
-}
-
 int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
     if (p->cut_valid && std::memcmp(key, p->cut_key, sizeof key) == 0) return CVQ_OK;
@@ -797,16 +740,6 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     p->cut_valid = false;
     if (!p->d_cutfix) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cutfix, h.size() * sizeof(int16_t)));
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cutfix, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
-    // balanced fixed-slab segments, off by default (CVQ_FIXSEG=1; measured 3-4% slower than the
-    // kernel's long-with-short row pairing on cfg 2, profiles/r03b)
-    static const bool fixseg = getenv("CVQ_FIXSEG") && atoi(getenv("CVQ_FIXSEG")) != 0;
-    std::vector<uint32_t> fs;
-    p->fseg_ok = fixseg && build_fixed_segments(h, n, compact_nt(), fs);
-    if (p->fseg_ok) {
-        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));   // the previous table may still be read
-        if (int rc = dev_alloc(&p->d_fseg, fs.size())) return rc;
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_fseg, fs.data(), fs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, p->stream));
-    }
     std::vector<int> cc;
     build_cell_counts(p->hvc, P, compact_tail_cap(), cc, &p->ccount_depth);
     const double blo[4] = {P.vmin, P.sg0, P.sg1, P.fg};      // k_compact's brackets' lower levels
@@ -925,8 +858,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         const bool tab = p->ccount_depth >= 0;
         const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
                             tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
-                            {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]},
-                            p->fseg_ok ? p->d_fseg : nullptr};
+                            {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]}};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
@@ -1377,7 +1309,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_fseg, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);

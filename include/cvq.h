@@ -264,7 +264,8 @@ int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* 
 
 /* Special functions on the device (known-answer tests against scipy):
  * fn 0 = t.ppf(u, nu) (student.py:102), 1 = norm.ppf (gaussian.py:44),
- * 2 = erf (utils/utils.py:20). */
+ * 2 = erf (utils/utils.py:20), 3 = t.ppf as the solve kernels' tables evaluate it for
+ * nu = 6 (integer-nu root, nu must be 6). */
 int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int64_t n,
                     double* out, int32_t mem);
 

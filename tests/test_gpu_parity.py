@@ -66,6 +66,19 @@ def test_special_functions_vs_scipy_and_mpmath():
     fin = np.isfinite(ref)
     assert np.array_equal(np.isfinite(got), fin)
     assert np.all(np.abs(got[fin] - ref[fin]) <= 1e-13 * np.abs(ref[fin]) + 1e-16)
+    # the device norm.ppf restates scipy's own (Cephes) ndtri: within 4 ulp of it everywhere
+    assert np.all(np.abs(got[fin] - ref[fin]) <= 4 * np.spacing(np.abs(ref[fin]))), \
+        np.max(np.abs(got[fin] - ref[fin]) / np.spacing(np.abs(ref[fin])))
+    # the solve kernels' t.ppf for nu = 6 (float-seeded root p^(1/6), no exp/log): same tables,
+    # ~1e-14 relative vs mpmath (far inside the 1e-8 node noise the VaR tolerates)
+    tr = k["truth_tppf_nu6"]
+    got = N.special("tppf6", ut, nu=6.0)
+    rel = np.abs(got - tr) / np.abs(tr)
+    assert rel.max() < 1e-13, rel.max()
+    ref6 = N.special("tppf", u, nu=6.0)
+    ok = np.isfinite(ref6) & (np.abs(ref6) > 1e-6)
+    assert np.array_equal(np.isfinite(N.special("tppf6", u, nu=6.0)), np.isfinite(ref6))
+    assert np.max(np.abs(N.special("tppf6", u, nu=6.0)[ok] - ref6[ok]) / np.abs(ref6[ok])) < 1e-13
     got = N.special("erf", k["erf_x"])
     assert np.max(np.abs(got - k["erf"])) <= 2.3e-16
 
@@ -131,3 +144,26 @@ def test_forecast_stage_matches_reference(case):
         else:
             got = engine.ukf_forecast(rc[:, d], n_in, p["a"], p["l"], p["q"])
             np.testing.assert_allclose(got, z["sigma_forecasts"][:, d], rtol=TABLE_RTOL)
+
+
+@pytest.mark.parametrize("strategy", ["compact", "sorted"])
+def test_node_count_measurement(strategy):
+    """cvq_plan_count_nodes (bench.py's FP64 roofline basis): a counted solve returns the same
+    VaR, and every date evaluates at least its first fixed slab and at most ~the reachable set
+    (COMPACT's block tail evaluates its whole last cell once, so a little above the path)."""
+    z = load_golden("cfg2_n64")
+    p = _plan(z, strategy=strategy)
+    ptf = float(z["ptf_mean"])
+    v0, _ = p.calc_var(ptf)
+    p.count_nodes(True)
+    v1, _ = p.calc_var(ptf)
+    nodes = p.nodes_evaluated()
+    p.count_nodes(False)
+    assert np.array_equal(v0, v1, equal_nan=True)
+    T = v0.size
+    assert 0.2 * p.reach_nodes * T < nodes <= 1.2 * p.reach_nodes * T, (nodes, p.reach_nodes, T)
+    p.calc_var(ptf)
+    with pytest.raises(RuntimeError):
+        p.nodes_evaluated()                 # the last solve was not counted
+    with pytest.raises(ValueError):
+        _plan(z, strategy="prefix").count_nodes(True)
