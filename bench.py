@@ -63,6 +63,9 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (vendor figure)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (nccl = RCCL over xGMI; gloo: the multi-rank path on "
+                         "fewer GPUs than ranks, ranks sharing devices round-robin -- a test rehearsal)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config number (1-5)")
@@ -114,9 +117,14 @@ def main():
     import torch.distributed as dist
     from copula_var import engine, synthetic
 
+    if a.backend == "gloo":                           # rehearsal: ranks may share a device
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     cfg = synthetic.baseline_configs()[a.config]
     if a.strategy == "auto":
         a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points)

@@ -534,7 +534,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int i = row[k];
         double A[2], B[2];
 #ifdef CVQ_ABL_TABLES
-        A[0] = A[1] = sx[i] * 0.5;
+        A[0] = A[1] = xv[k] * 0.5;                                  // ablation: z = x / 2 (finite)
         B[0] = B[1] = 1.0;
 #else
         table_pair<COP, MSM, FUSED, (COP == CVQ_STUDENT && PM == 8) ? 6 : 0>(S, a, tA, tB, t, i, A, B);
