@@ -57,6 +57,8 @@ struct SolveConst {
     double ptf_mean;
     double* fin_var;              // nullptr: no fused finalize (sharded / PREFIX)
     int* fin_err;                 // [4]: error, kstop, N, workgroup ticket (0 between launches)
+    int exact_walk;               // every bracket's bisection points are exact dyadics (dyadic_walk_ok):
+                                  // COMPACT's tail walks its remaining levels in closed form, one per lane
 };
 
 struct alignas(16) Header {       // per-rank solve summary, all-gathered across ranks

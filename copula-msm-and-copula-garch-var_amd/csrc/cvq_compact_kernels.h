@@ -96,9 +96,6 @@ constexpr uint32_t kTlRowMask = 0x7FFu;
 constexpr int kTlColShift = 11;
 constexpr uint32_t kTlGroupEnd = 1u << 31;
 constexpr int kNoPos = 0x7FFFFFFF;                  // "no such position" in the crossing search
-#ifndef CVQ_TAIL_VSTAR
-#define CVQ_TAIL_VSTAR 1
-#endif
 
 #ifndef CVQ_COMPACT_PRIO
 #define CVQ_COMPACT_PRIO 0
@@ -867,65 +864,70 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const unsigned long long bc = __ballot(mc < NPT), bz = __ballot(mz < NPT);
         int* ew = (int*)(red + parity * (3 * (NT / 64)));         // the other reduction half: 2 ints / wave
         parity ^= 1;
-        // the first flagged thread of the wave holds the wave's first crossing; its position
-        // and node word go to LDS.  The leader then compares each mid with that node's v*
-        // (loaded once from the plan's sorted v* list: CVQ_TAIL_VSTAR = 1, measured faster) or
-        // evaluates the membership test x_j <= (mid - x_r w1) / w0 itself per level (= 0)
+        // the first flagged thread of the wave holds the wave's first crossing; its position goes
+        // to LDS, and the walk compares each mid with that node's v* from the plan's sorted list
+        // (measured faster than re-evaluating the membership test x_j <= (mid - x_r w1) / w0)
         const int lc = bc ? (int)__builtin_ctzll(bc) : 0, lz = bz ? (int)__builtin_ctzll(bz) : 0;
         const int mcl = __shfl(mc, lc, 64), mzl = __shfl(mz, lz, 64);
-        uint32_t wc = 0u, wz = 0u;
-#pragma unroll
-        for (int m = 0; m < NPT; ++m) {
-            wc = m == mc ? wd[m] : wc;
-            wz = m == mz ? wd[m] : wz;
-        }
-        const uint32_t wcl = (uint32_t)__shfl((int)wc, lc, 64), wzl = (uint32_t)__shfl((int)wz, lz, 64);
         if (lane == 0) {
             int* e = ew + 4 * (tid >> 6);
             e[0] = bc ? ((tid >> 6) * 64 + lc) * NPT + mcl : kNoPos;
-            e[1] = (int)wcl;
             e[2] = bz ? ((tid >> 6) * 64 + lz) * NPT + mzl : kNoPos;
-            e[3] = (int)wzl;
         }
         __syncthreads();
         stamp(29);
-        if (tid == leader) {
+        // exact dyadic bisection points (host check, P.exact_walk): wave 0 walks the remaining
+        // levels in closed form, lane l = level it + l; else lane 0 walks them one by one
+        const bool exact = P.exact_walk != 0;
+        if (exact ? tid < 64 : tid == leader) {
             int ec = kNoPos, ez = kNoPos;
-            uint32_t nc = 0u, nz_ = 0u;
 #pragma unroll
             for (int w = 0; w < NT / 64; ++w) {                   // waves in position order: first wins
                 const int* e = ew + 4 * w;
-                if (ec == kNoPos && e[0] != kNoPos) { ec = e[0]; nc = (uint32_t)e[1]; }
-                if (ez == kNoPos && e[2] != kNoPos) { ez = e[2]; nz_ = (uint32_t)e[3]; }
+                if (ec == kNoPos && e[0] != kNoPos) ec = e[0];
+                if (ez == kNoPos && e[2] != kNoPos) ez = e[2];
             }
             // kind: 0 = every mid (F just above lo already decides), 1 = no mid, 2 = mids at or
-            // above the node's threshold
+            // above the node's threshold (v* loaded from the plan's sorted list)
             const int kc = !(Flo < P.obj) ? 0 : (ec == kNoPos ? 1 : 2);
             const int kz = (Flo != 0.0) ? 0 : (ez == kNoPos ? 1 : 2);
-#if !CVQ_TAIL_VSTAR
-            const double xjc = sx[(nc >> kTlColShift) & kTlRowMask], levc = sx[nc & kTlRowMask] * S.w1;
-            const double xjz = sx[(nz_ >> kTlColShift) & kTlRowMask], levz = sx[nz_ & kTlRowMask] * S.w1;
-#else
-            (void)nc;
-            (void)nz_;
-#endif
-#if CVQ_TAIL_VSTAR                                            // A/B: compare mids with loaded v* values
             const double vcs = kc == 2 ? G.tvs[ps + ec] : 0.0, vzs = kz == 2 ? G.tvs[ps + ez] : 0.0;
-#endif
-            for (; it < P.K; ++it) {
-                const double mid = (lo + hi) / 2;
-                sn[it] = mid;
-                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-#if CVQ_TAIL_VSTAR
-                const bool geq = kc == 0 || (kc == 2 && mid >= vcs);
-                const bool nz = kz == 0 || (kz == 2 && mid >= vzs);
-#else
-                const bool geq = kc == 0 || (kc == 2 && xjc <= inner_coord(S, mid, levc));   // !(F(mid) < obj)
-                const bool nz = kz == 0 || (kz == 2 && xjz <= inner_coord(S, mid, levz));    // F(mid) != 0
-#endif
-                if (nz) mask |= (1ull << it);
-                ustack = !geq;
-                if (ustack) lo = mid; else hi = mid;
+            if (exact) {
+                // every decision is "mid >= v_c" (hi = mid) on one dyadic grid, so after the R remaining
+                // levels the bracket is the cell (lo + c wR, lo + (c + 1) wR] holding v_c (c = 0: every mid
+                // decided high, c = 2^R - 1: none did), and level l's bracket is that cell's ancestor
+                // c >> (R - l): mid_l = lo + (2 (c >> (R - l)) + 1) w 2^-(l+1), all exact (host-checked)
+                const int R = P.K - it;                            // 1 <= R <= 52
+                const double w = hi - lo, wR = ldexp(w, -R), top = ldexp(1.0, R) - 1.0;
+                double c = kc == 0 ? 0.0 : top;
+                if (kc == 2) {
+                    c = fmin(fmax(ceil((vcs - lo) / wR) - 1.0, 0.0), top);   // within 1 of the cell
+                    if (c > 0.0 && !(fma(c, wR, lo) < vcs)) c -= 1.0;
+                    else if (c < top && !(vcs <= fma(c + 1.0, wR, lo))) c += 1.0;
+                }
+                const bool act = lane < R;
+                const double cl = floor(ldexp(c, lane - R));
+                const double mid = fma(2.0 * cl + 1.0, ldexp(w, -(lane + 1)), lo);
+                if (act) sn[it + lane] = mid;
+                const unsigned long long bz = __ballot(act && (kz == 0 || (kz == 2 && mid >= vzs)));
+                const unsigned long long bt = __ballot(act && !(ldexp(w, -lane) > P.tol));
+                if (nt < 0 && bt) nt = it + (int)__builtin_ctzll(bt);
+                mask |= bz << it;
+                const double lo0 = lo;
+                lo = fma(c, wR, lo0);
+                hi = fma(c + 1.0, wR, lo0);
+                it = P.K;
+            } else {
+                for (; it < P.K; ++it) {
+                    const double mid = (lo + hi) / 2;
+                    sn[it] = mid;
+                    if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+                    const bool geq = kc == 0 || (kc == 2 && mid >= vcs);
+                    const bool nz = kz == 0 || (kz == 2 && mid >= vzs);
+                    if (nz) mask |= (1ull << it);
+                    ustack = !geq;
+                    if (ustack) lo = mid; else hi = mid;
+                }
             }
         }
     } else if (it < P.K) {

@@ -1003,6 +1003,29 @@ bool materialised(const cvq_plan* p) {
     return p->strategy == CVQ_STRATEGY_PREFIX || sorted_family(p);
 }
 
+// The bisection of bracket (lo, hi] over K levels visits only exact dyadic points when the width
+// W = hi - lo is a power of two and lo is an integer multiple N of q = W 2^-K with |N| + 2^K < 2^53:
+// every cell end lo + k q (0 <= k <= 2^K) is then N' q with |N'| < 2^53, so (lo + hi) / 2 of the
+// reference (calc_var_class.py:281) is exact at every level and the level-l bracket of a date is
+// lo + c 2^(K-l) q with c read off the final cell (COMPACT's closed-form tail walk).
+bool dyadic_bracket_ok(double lo, double hi, int K) {
+    if (!(std::isfinite(lo) && std::isfinite(hi) && hi > lo) || K < 1 || K > 52) return false;
+    const double W = hi - lo;
+    if (W + lo != hi || hi - W != lo) return false;                // the width itself exact
+    int e;
+    if (std::frexp(W, &e) != 0.5) return false;                    // W = 2^(e-1)
+    const double q = std::ldexp(W, -K);
+    if (!(q > 0.0) || !std::isnormal(q)) return false;
+    const double N = lo / q;                                       // exact: q is a power of two
+    return N == std::floor(N) && std::fabs(N) + std::ldexp(1.0, K) < std::ldexp(1.0, 53);
+}
+
+bool dyadic_walk_ok(const cvq_solve_args& a, int K) {
+    // k_compact's brackets (calc_var_class.py:137-149): (vmin, sg0], (sg0, fg], (sg1, vmax], (fg, sg1]
+    return dyadic_bracket_ok(a.min_var, a.second_guess_lo, K) && dyadic_bracket_ok(a.second_guess_lo, a.first_guess, K) &&
+           dyadic_bracket_ok(a.second_guess_hi, a.max_var, K) && dyadic_bracket_ok(a.first_guess, a.second_guess_hi, K);
+}
+
 SolveConst solve_const(const cvq_solve_args& a, int K) {
     SolveConst P;
     P.obj = a.obj_var;
@@ -1018,6 +1041,8 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.ptf_mean = a.ptf_mean;
     P.fin_var = nullptr;
     P.fin_err = nullptr;
+    static const bool serial_walk = getenv("CVQ_SERIAL_WALK") && atoi(getenv("CVQ_SERIAL_WALK")) != 0;   // A/B
+    P.exact_walk = !serial_walk && dyadic_walk_ok(a, K) ? 1 : 0;
     return P;
 }
 

@@ -11,6 +11,8 @@ from copula_var import _native as N
 
 STRAT = sys.argv[sys.argv.index("--strategy") + 1] if "--strategy" in sys.argv else "direct"
 cfg = synthetic.baseline_configs()[int(sys.argv[sys.argv.index("--config") + 1]) if "--config" in sys.argv else 2]
+if "--dates" in sys.argv:                      # the first N dates only (e.g. 1: one date alone on the GPU)
+    cfg = cfg.with_(T=int(sys.argv[sys.argv.index("--dates") + 1]))
 rets = synthetic.simulate_returns(cfg)
 mean, ptf, centred, T = tables.insample_split(rets, cfg.n_in, cfg.weights)
 ipt, uvs, ggp = (tables.msm_integration_params(centred, cfg.n_in, cfg.msm_params, cfg.k, cfg.num_points)
