@@ -124,6 +124,9 @@ struct CompactGeom {
     const uint32_t* tlist;
     const double* tvs;
     int bstart[4];
+    // with ccount: [4][2^cdepth][n] per-row cuts cnt_r(mid) of every bisection cell the levels split
+    // (heap nodes 1 .. 2^cdepth - 1; date-independent, host-built); nullptr: the levels search the grid
+    const int16_t* kcut;
 };
 
 // ------------------------------------------------------------------ reductions
@@ -160,6 +163,38 @@ __device__ __forceinline__ double wave_incl_scan_f64(double v) {
     v += dpp_f64z<0x142, 0xA>(v);
     v += dpp_f64z<0x143, 0xC>(v);
     return v;
+}
+
+// The remaining R = K - it bisection levels of a date in closed form (P.exact_walk: every bracket's
+// bisection points are exact dyadics, host-checked by dyadic_walk_ok).  Every decision is "mid >=
+// v_c" (hi = mid), so after R levels the bracket is the cell (lo + c wR, lo + (c + 1) wR] holding v_c
+// (kc 0: every mid decides high, c = 0; kc 1: none does, c = 2^R - 1), and level l's bracket is that
+// cell's ancestor c >> (R - l): mid_l = lo + (2 (c >> (R - l)) + 1) w 2^-(l+1), all exact.  The Q4
+// bit of level l is mid_l >= v_z (kz 0: always, 1: never).  Called by all 64 lanes of one wave
+// (lane l = level it + l); lo, hi, it, nt, mask come out identical in every lane.
+__device__ __forceinline__ void dyadic_walk(const SolveConst& P, int kc, double vcs, int kz, double vzs, double& lo,
+                                            double& hi, int& it, int& nt, uint64_t& mask, double* sn) {
+    const int lane = threadIdx.x & 63;
+    const int R = P.K - it;                                    // 1 <= R <= 52
+    const double w = hi - lo, wR = ldexp(w, -R), top = ldexp(1.0, R) - 1.0;
+    double c = kc == 0 ? 0.0 : top;
+    if (kc == 2) {
+        c = fmin(fmax(ceil((vcs - lo) / wR) - 1.0, 0.0), top);   // within 1 of the cell
+        if (c > 0.0 && !(fma(c, wR, lo) < vcs)) c -= 1.0;
+        else if (c < top && !(vcs <= fma(c + 1.0, wR, lo))) c += 1.0;
+    }
+    const bool act = lane < R;
+    const double cl = floor(ldexp(c, lane - R));
+    const double mid = fma(2.0 * cl + 1.0, ldexp(w, -(lane + 1)), lo);
+    if (act) sn[it + lane] = mid;
+    const unsigned long long bz = __ballot(act && (kz == 0 || (kz == 2 && mid >= vzs)));
+    const unsigned long long bt = __ballot(act && !(ldexp(w, -lane) > P.tol));
+    if (nt < 0 && bt) nt = it + (int)__builtin_ctzll(bt);
+    mask |= bz << it;
+    const double lo0 = lo;
+    lo = fma(c, wR, lo0);
+    hi = fma(c + 1.0, wR, lo0);
+    it = P.K;
 }
 
 // Block-wide exclusive scan of v; *total = sum over the block.  One barrier.
@@ -520,6 +555,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int w = min(tid + NT * k, (kCutLds / 2) * n - 1);
         cv[k] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
     }
+    // the first bisection level's per-row cuts of all four brackets (host table G.kcut, heap node 1)
+    int krt[4][RPT];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+            krt[b][k] = (G.kcut && G.ccount) ? G.kcut[(((size_t)b << G.cdepth) + 1) * n + min(tid + NT * k, n - 1)] : 0;
 
     // ---- tables: index i -> row record i (axis 0) and column record i (axis 1)
     const int q = MSM ? S.q : 1;
@@ -745,6 +787,15 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     const bool tabc = G.ccount != nullptr;
     const int* cc = tabc ? G.ccount + ((size_t)max(bsel, 0) << (G.cdepth + 1)) : nullptr;
     const int hend = tabc ? 2 << G.cdepth : 0;                   // heap nodes 1 .. 2^(cdepth+1) - 1
+    // the levels' per-row cuts from the host table (tabulated cells: heap nodes < 2^cdepth), the
+    // two children's loaded one level ahead; the first level's loaded with the bracket
+    const bool tcut = tabc && G.kcut != nullptr && bsel >= 0;
+    const int16_t* kc0 = tcut ? G.kcut + ((size_t)bsel << G.cdepth) * n : nullptr;
+    const int kcn = tcut ? 1 << G.cdepth : 0;
+    int kmt[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+        kmt[k] = bsel == 0 ? krt[0][k] : bsel == 1 ? krt[1][k] : bsel == 2 ? krt[2][k] : krt[3][k];
     int hc = 1;
     int nbr_next = !tabc ? 1 << 30 : (bsel < 0 || hc >= hend) ? 0 : cc[hc];
     int ps = (tabc && bsel >= 0) ? G.bstart[bsel] : 0;           // the cell's first sorted position
@@ -758,13 +809,21 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         // the children's counts, loaded while the level runs (depth cdepth: all <= kTailCap)
         const int c_lo = (tabc && 2 * hc < hend) ? cc[2 * hc] : 0;
         const int c_hi = (tabc && 2 * hc + 1 < hend) ? cc[2 * hc + 1] : 0;
-        int kM[RPT];
+        int kM[RPT], kml[RPT], kmh[RPT];
+        const bool tnext = tcut && 2 * hc + 1 < kcn;               // both children tabulated: fetch now
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int rr = own[k] ? row[k] : 0;
+            kml[k] = tnext ? kc0[(size_t)(2 * hc) * n + rr] : 0;
+            kmh[k] = tnext ? kc0[(size_t)(2 * hc + 1) * n + rr] : 0;
+        }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
 #ifdef CVQ_ABL_CNT
             kM[k] = own[k] ? (kLo[k] + kHi[k]) >> 1 : 0;
 #else
-            kM[k] = own[k] ? grid_count(sx, bk, G, inner_coord(S, mid, lev[k]), kLo[k], kHi[k]) : 0;   // Q10
+            kM[k] = !own[k] ? 0 : (tcut && hc < kcn) ? kmt[k]
+                  : grid_count(sx, bk, G, inner_coord(S, mid, lev[k]), kLo[k], kHi[k]);   // Q10
 #endif
             ka[k] = ustack ? kLo[k] : kM[k];
             kb[k] = ustack ? kM[k] : kHi[k];
@@ -792,6 +851,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const double Fn = (slab_lower == prevU) ? prev + val : prev - val;   // adjust_integral
         if (Fn != 0.0) mask |= (1ull << it);
         ustack = Fn < P.obj;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) kmt[k] = ustack ? kmh[k] : kml[k];
         if (ustack) {
             lo = mid;
             nbr_next = tabc ? c_hi : Nbr - Nlow;
@@ -893,30 +954,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             const int kz = (Flo != 0.0) ? 0 : (ez == kNoPos ? 1 : 2);
             const double vcs = kc == 2 ? G.tvs[ps + ec] : 0.0, vzs = kz == 2 ? G.tvs[ps + ez] : 0.0;
             if (exact) {
-                // every decision is "mid >= v_c" (hi = mid) on one dyadic grid, so after the R remaining
-                // levels the bracket is the cell (lo + c wR, lo + (c + 1) wR] holding v_c (c = 0: every mid
-                // decided high, c = 2^R - 1: none did), and level l's bracket is that cell's ancestor
-                // c >> (R - l): mid_l = lo + (2 (c >> (R - l)) + 1) w 2^-(l+1), all exact (host-checked)
-                const int R = P.K - it;                            // 1 <= R <= 52
-                const double w = hi - lo, wR = ldexp(w, -R), top = ldexp(1.0, R) - 1.0;
-                double c = kc == 0 ? 0.0 : top;
-                if (kc == 2) {
-                    c = fmin(fmax(ceil((vcs - lo) / wR) - 1.0, 0.0), top);   // within 1 of the cell
-                    if (c > 0.0 && !(fma(c, wR, lo) < vcs)) c -= 1.0;
-                    else if (c < top && !(vcs <= fma(c + 1.0, wR, lo))) c += 1.0;
-                }
-                const bool act = lane < R;
-                const double cl = floor(ldexp(c, lane - R));
-                const double mid = fma(2.0 * cl + 1.0, ldexp(w, -(lane + 1)), lo);
-                if (act) sn[it + lane] = mid;
-                const unsigned long long bz = __ballot(act && (kz == 0 || (kz == 2 && mid >= vzs)));
-                const unsigned long long bt = __ballot(act && !(ldexp(w, -lane) > P.tol));
-                if (nt < 0 && bt) nt = it + (int)__builtin_ctzll(bt);
-                mask |= bz << it;
-                const double lo0 = lo;
-                lo = fma(c, wR, lo0);
-                hi = fma(c + 1.0, wR, lo0);
-                it = P.K;
+                dyadic_walk(P, kc, vcs, kz, vzs, lo, hi, it, nt, mask, sn);
             } else {
                 for (; it < P.K; ++it) {
                     const double mid = (lo + hi) / 2;

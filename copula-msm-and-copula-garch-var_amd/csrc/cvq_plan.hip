@@ -165,6 +165,8 @@ struct cvq_plan {
     double* d_tvs = nullptr;     // [n (n - 1)] = hvc on the device
     int bstart[4] = {0, 0, 0, 0};   // ub(bracket lower) in hvc for the cached solve arguments
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
+    int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
+    bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
     // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
@@ -751,6 +753,32 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
         if (int rc = dev_alloc(&p->d_ccount, cc.size())) return rc;
         CVQ_HIP_CHECK(hipMemcpyAsync(p->d_ccount, cc.data(), cc.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
     }
+    // per-row cuts of every tabulated bisection cell's mid (the levels' cnt_r(mid) without a grid
+    // search): [4][2^D][n] int16, heap node h of bracket b at (b << D) + h; bounded to 4 MB
+    static const bool no_kcut = getenv("CVQ_LEVEL_CUTS") && atoi(getenv("CVQ_LEVEL_CUTS")) == 0;   // A/B switch
+    const int D = p->ccount_depth;
+    p->kcut_ok = !no_kcut && D >= 1 && ((size_t)4 << D) * n * sizeof(int16_t) <= ((size_t)4 << 20);
+    if (p->kcut_ok) {
+        std::vector<int16_t> kc(((size_t)4 << D) * n, 0);
+        const double br[4][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.sg1, P.vmax}, {P.fg, P.sg1}};
+        for (int b = 0; b < 4; ++b) {
+            std::vector<double> clo(1 << D), chi(1 << D);       // heap cell bounds, as the kernel halves them
+            clo[1] = br[b][0];
+            chi[1] = br[b][1];
+            for (int h = 1; h < (1 << D); ++h) {
+                const double mid = (clo[h] + chi[h]) / 2;
+                if (2 * h + 1 < (1 << D)) {
+                    clo[2 * h] = clo[h]; chi[2 * h] = mid;
+                    clo[2 * h + 1] = mid; chi[2 * h + 1] = chi[h];
+                }
+                int16_t* dst = kc.data() + (((size_t)b << D) + h) * n;
+                for (int r = 0; r < n; ++r) dst[r] = (int16_t)host_cnt(p->hx, p->hx[r] * p->S.w1, p->S.w0, mid);
+            }
+        }
+        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+        if (int rc = dev_alloc(&p->d_kcut, kc.size())) return rc;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_kcut, kc.data(), kc.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
+    }
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     std::memcpy(p->cut_key, key, sizeof key);
     p->cut_valid = true;
@@ -824,6 +852,8 @@ SortedGeom sorted_geom(const cvq_plan* p, bool solve) {
     G.trw0 = p->d_trw0;
     G.layout = p->layout;
     G.trw2 = p->d_trw2;
+    G.tidx = p->d_sidx;
+    G.tvs = p->d_svs;
     return G;
 }
 
@@ -858,7 +888,8 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         const bool tab = p->ccount_depth >= 0;
         const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
                             tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
-                            {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]}};
+                            {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]},
+                            (tab && p->kcut_ok) ? p->d_kcut : nullptr};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
@@ -1334,7 +1365,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);

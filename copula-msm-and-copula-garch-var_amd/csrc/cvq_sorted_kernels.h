@@ -85,6 +85,10 @@ struct SortedGeom {
     const uint32_t* trw0;
     const uint32_t* trw2;
     int layout;            // node-word layout (sorted_pack): kLay2W for folded Student records
+    // the v*-sorted node words and v* (the solve order above is row-major inside each segment
+    // between slab ends; the tail's prefix scan needs the tail cell's nodes in v* order)
+    const uint32_t* tidx;
+    const double* tvs;
 };
 
 // chunk geometry of a sweep over sorted positions [ps, pe): thread t takes [a0 + t L, a0 + (t + 1) L)
@@ -872,14 +876,81 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     // ---- tail: the bracket's <= TCAP nodes -> LDS, wave 0 finishes the levels
     if (it < P.K) {
         const int tot = phi - plo;
+        // exact walk: the cell's nodes in v* order (same node set: plo, phi are segment boundaries)
+        const uint32_t* tix = P.exact_walk ? G.tidx : G.idx;
+        const double* tv = P.exact_walk ? G.tvs : G.vs;
         for (int e = tid; e < tot; e += NT) {
-            const uint32_t c = G.idx[plo + e];
-            tail[e] = make_double2(G.vs[plo + e], fast ? node_fast(c) : node_generic(c));
+            const uint32_t c = tix[plo + e];
+            tail[e] = make_double2(tv[plo + e], fast ? node_fast(c) : node_generic(c));
         }
         __syncthreads();
         stamp(29);
         nodes += tot;
-        if (tid < 64) {
+        if (tid < 64 && P.exact_walk) {
+            // exact dyadic brackets: lane holds the tail's positions lane TPL + m (in order); one level by
+            // masked sums if none ran yet (the reference's first level may subtract a slab it never
+            // added, Q1), then F at every tie-group end from one prefix scan (F = prev + prefix when the
+            // last level moved lo, else prev - (cell total - prefix): adjust_integral's chain), the two
+            // crossing thresholds v_c (first end with !(F < obj)) and v_z (first with F != 0), and the
+            // remaining levels in closed form (dyadic_walk) -- the COMPACT block tail's scheme
+            double tx[TPL], ty[TPL];
+#pragma unroll
+            for (int m = 0; m < TPL; ++m) {
+                const int e = lane * TPL + m;
+                const double2 v = e < tot ? tail[e] : make_double2(__builtin_nan(""), 0.0);
+                tx[m] = v.x;
+                ty[m] = v.y;
+            }
+            if (it == 0) {
+                const double mid = (lo + hi) / 2;
+                if (tid == 0) sn[it] = mid;
+                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
+                const double a0 = ustack ? lo : mid, b0 = ustack ? mid : hi;   // slab (a0, b0]
+                double p = 0.0;
+#pragma unroll
+                for (int m = 0; m < TPL; ++m) p += (tx[m] > a0 && tx[m] <= b0) ? ty[m] : 0.0;
+                const double val = wave_sum(p);
+                const double slab_lower = ustack ? lo : mid;
+                const double Fn = (slab_lower == prevU) ? prev + val : prev - val;
+                if (Fn != 0.0) mask |= (1ull << it);
+                ustack = Fn < P.obj;
+                if (ustack) lo = mid; else hi = mid;
+                prev = Fn;
+                prevU = mid;
+                ++it;
+#pragma unroll
+                for (int m = 0; m < TPL; ++m)                     // the cell's entries only
+                    if (!(tx[m] > lo && tx[m] <= hi)) ty[m] = 0.0;
+            }
+            if (it < P.K) {
+                double run = 0.0;
+#pragma unroll
+                for (int m = 0; m < TPL; ++m) run += (tx[m] > lo && tx[m] <= hi) ? ty[m] : 0.0;
+                const double incl = wave_incl_scan_f64(run);
+                const double Stot = readlane_f64(incl, 63);
+                const double Flo = ustack ? prev : prev - Stot;   // F just above lo
+                const double nx = __shfl(tx[0], (lane + 1) & 63, 64);
+                double pa = incl - run;
+                int mc = TPL, mz = TPL;
+                double vc = 0.0, vz = 0.0;
+#pragma unroll
+                for (int m = 0; m < TPL; ++m) {
+                    const bool in = tx[m] > lo && tx[m] <= hi;
+                    pa += in ? ty[m] : 0.0;
+                    const double tn = m + 1 < TPL ? tx[m + 1] : nx;
+                    const bool gend = in && (lane * TPL + m == tot - 1 || !(tn <= tx[m]));   // last of its v*
+                    const double Fv = ustack ? prev + pa : prev - (Stot - pa);
+                    if (gend && mc == TPL && !(Fv < P.obj)) { mc = m; vc = tx[m]; }
+                    if (gend && mz == TPL && Fv != 0.0) { mz = m; vz = tx[m]; }
+                }
+                const unsigned long long bc = __ballot(mc < TPL), bz = __ballot(mz < TPL);
+                const int kc = !(Flo < P.obj) ? 0 : (bc ? 2 : 1);
+                const int kz = (Flo != 0.0) ? 0 : (bz ? 2 : 1);
+                const double vcs = __shfl(vc, bc ? (int)__builtin_ctzll(bc) : 0, 64);
+                const double vzs = __shfl(vz, bz ? (int)__builtin_ctzll(bz) : 0, 64);
+                dyadic_walk(P, kc, vcs, kz, vzs, lo, hi, it, nt, mask, sn);
+            }
+        } else if (tid < 64) {
             double tx[TPL], ty[TPL];
 #pragma unroll
             for (int m = 0; m < TPL; ++m) {
