@@ -393,8 +393,14 @@ __global__ __launch_bounds__(64) void k_msm_windows(MsmParamsN PN, const double*
 // 2^k x 2^k mat-vecs instead of n filter steps.  All factors are non-negative; each is kept
 // at a common scale of its own (a positive factor cancels in the final normalisation), so
 // the forecasts agree with the step-by-step filter to ~1e-14 relative.
-constexpr int kScanB = 32;       // steps per block
-constexpr int kScanC = 16;       // blocks per superblock
+#ifndef CVQ_SCAN_B
+#define CVQ_SCAN_B 32
+#endif
+#ifndef CVQ_SCAN_C
+#define CVQ_SCAN_C 16
+#endif
+constexpr int kScanB = CVQ_SCAN_B;   // steps per block (the block scan's serial chain)
+constexpr int kScanC = CVQ_SCAN_C;   // blocks per superblock (the superblock scan's serial chain)
 
 // v <- A v for a quad-resident state vector (the transition of calc_prob.py:91-101 as k
 // Kronecker butterflies; A is symmetric, so this is also v^T A for a row vector)
