@@ -393,11 +393,13 @@ __global__ __launch_bounds__(64) void k_msm_windows(MsmParamsN PN, const double*
 // 2^k x 2^k mat-vecs instead of n filter steps.  All factors are non-negative; each is kept
 // at a common scale of its own (a positive factor cancels in the final normalisation), so
 // the forecasts agree with the step-by-step filter to ~1e-14 relative.
+// B = 16, C = 8 (r03): e2e 16.7-16.8 M -> 18.1-18.4 M VaR-dates/s vs B = 32, C = 16 (profiles/r03p); a
+// n_in = 1135 window then takes up to ~10 factors instead of 5, but both serial chains halve
 #ifndef CVQ_SCAN_B
-#define CVQ_SCAN_B 32
+#define CVQ_SCAN_B 16
 #endif
 #ifndef CVQ_SCAN_C
-#define CVQ_SCAN_C 16
+#define CVQ_SCAN_C 8
 #endif
 constexpr int kScanB = CVQ_SCAN_B;   // steps per block (the block scan's serial chain)
 constexpr int kScanC = CVQ_SCAN_C;   // blocks per superblock (the superblock scan's serial chain)

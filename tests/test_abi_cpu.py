@@ -125,10 +125,10 @@ def test_new_entry_points_validate_on_the_host():
     n = C.c_int64()
     assert lib.cvq_msm_tables_scratch(2, 4, 1135, 1000, C.byref(n)) == N.CVQ_OK
     # cond, filt, then the scan filter's buffers per asset (window-end prefixes, window-start
-    # suffix row sums, 66 block products, 5 superblocks of 16 prefixes + 16 suffixes), err
-    # word, then one error flag (int) per asset and block of 32 steps (2 x 67)
-    scan = 1000 * 256 + 1000 * 16 + (2134 // 32) * 256 + 2 * 5 * 16 * 256
-    assert n.value == 2 * 2134 * 16 + 2 * 1000 * 16 + 2 * scan + 2 + (2 * 67 + 1) // 2
+    # suffix row sums, 133 block products of 16 steps, 17 superblocks of 8 prefixes + 8 suffixes),
+    # err word, then one error flag (int) per asset and block (2 x 134)
+    scan = 1000 * 256 + 1000 * 16 + (2134 // 16) * 256 + 2 * 17 * 8 * 256
+    assert n.value == 2 * 2134 * 16 + 2 * 1000 * 16 + 2 * scan + 2 + (2 * 134 + 1) // 2
     assert lib.cvq_msm_tables_scratch(4, 4, 1135, 1000, C.byref(n)) == N.CVQ_ERR_INVALID
     prm = np.array([0.45, 1.2, 3.0, 0.3, 0.5, 1.2, 3.0, 0.3])
     smap = np.zeros(32, dtype=np.int32)
