@@ -39,12 +39,14 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None) -> str:
     among those that run it: COMPACT for 2-asset MSM (cfg 2: 20.3M vs SORTED 16.4M
     VaR-dates/s), SORTED for 2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for
     3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
-    bounds the choice: 3-D SORTED takes n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
+    bounds the choice: 2-D SORTED takes n <= 512 (larger 2-D grids go to COMPACT, which
+    hands n > 2048 to k_direct), 3-D SORTED n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
     takes n > 255.  SORTED and PREFIX hold the nodes with level <= v_cap only;
     QuadraturePlan(strategy="auto") routes a query above v_cap to an unrestricted
     sibling plan (COMPACT / DIRECT in 2-D, SORTED with v_cap at the grid's top in 3-D)."""
     if dim == 2:
-        return "compact" if model == "msm" else "sorted"
+        # SORTED holds 2-D grids up to SORTED_MAX_N[2]; COMPACT runs larger ones (k_direct past 2048)
+        return "compact" if model == "msm" or (n is not None and n > SORTED_MAX_N[2]) else "sorted"
     if n is None or n <= SORTED_MAX_N[3]:
         return "sorted"
     raise ValueError(f"3-asset grids support num_points <= {SORTED_MAX_N[3]} (SORTED), got {n}")
@@ -86,6 +88,8 @@ class QuadraturePlan:
         self._auto = strategy == "auto"
         self._wide: Optional["QuadraturePlan"] = None       # unrestricted sibling (auto, level > v_cap)
         self._dates = None                                  # last set_dates / set_dates_device arguments
+        self._stream, self._timing, self._counting = None, False, False   # forwarded to the sibling
+        self._last: Optional["QuadraturePlan"] = None       # plan of the last device solve (solve_status)
         if strategy == "auto":
             strategy = auto_strategy(model, self.dim, self._x.size)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
@@ -135,7 +139,16 @@ class QuadraturePlan:
             if self._dates is not None:
                 kind, args = self._dates
                 (self._wide.set_dates if kind == "host" else self._wide.set_dates_device)(*args)
+            self._wide.set_stream(self._stream)
+            self._wide.enable_timing(self._timing)
+            self._wide.count_nodes(self._counting)
         return self._wide._route(top)
+
+    @staticmethod
+    def _top(args: N.CvqSolveArgs) -> float:
+        """The highest level a solve with these arguments can query."""
+        return max(args.first_guess, args.second_guess_lo, args.second_guess_hi, args.max_var, args.min_var,
+                   args.lower)
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -146,6 +159,9 @@ class QuadraturePlan:
     def set_stream(self, stream_handle: Optional[int]) -> None:
         """Launch on this HIP stream from now on (0 / None = the null stream, torch's default)."""
         N.check(N.lib().cvq_plan_set_stream(self._h, C.c_void_p(stream_handle or 0)), "cvq_plan_set_stream")
+        self._stream = stream_handle
+        if self._wide is not None:
+            self._wide.set_stream(stream_handle)
 
     KERNELS = {"tables": 0, "mass": 1, "solve": 2, "finalize": 3, "slab": 4}
 
@@ -159,6 +175,9 @@ class QuadraturePlan:
             for k in on:
                 mask |= 1 << self.KERNELS[k]
         N.check(N.lib().cvq_plan_timing(self._h, mask), "cvq_plan_timing")
+        self._timing = on if (on is True or on is False) else tuple(on)
+        if self._wide is not None:
+            self._wide.enable_timing(self._timing)
 
     def kernel_time(self, kind: str) -> Tuple[float, int]:
         """(total milliseconds, launches) of one kernel kind since enable_timing()."""
@@ -171,6 +190,9 @@ class QuadraturePlan:
         """Record, in the following solves, how many quadrature nodes each date evaluates
         (COMPACT / SORTED / SWEEP; measurement aid, slower -- never in a timed run)."""
         N.check(N.lib().cvq_plan_count_nodes(self._h, 1 if on else 0), "cvq_plan_count_nodes")
+        self._counting = bool(on)
+        if self._wide is not None:
+            self._wide.count_nodes(on)
 
     def nodes_evaluated(self) -> int:
         """Nodes evaluated by the last counted solve, summed over its dates."""
@@ -233,9 +255,7 @@ class QuadraturePlan:
                  **consts) -> Tuple[np.ndarray, int]:
         """Drop-in for calc_var (calc_var_class.py:95-177): returns (VaR (T,), iterations)."""
         args = solve_args(ptf_mean, obj_var, first_guess, second_guess, **consts)
-        top = max(args.first_guess, args.second_guess_lo, args.second_guess_hi, args.max_var, args.min_var,
-                  args.lower)
-        target = self._route(top)
+        target = self._route(self._top(args))
         if target is not self:
             return target.calc_var(ptf_mean, obj_var, first_guess, second_guess, **consts)
         out = np.empty(self.T)
@@ -248,7 +268,12 @@ class QuadraturePlan:
         """calc_var into a device buffer.  check=False: in stream order, no host
         synchronisation and no convergence check (call solve_status() to check);
         check=True: synchronises, widens the bisection budget if a date needed more
-        iterations (non-dyadic guesses) and returns the iteration count."""
+        iterations (non-dyadic guesses) and returns the iteration count.  A plan built with
+        strategy "auto" routes levels above v_cap to its unrestricted sibling, as calc_var does."""
+        target = self._route(self._top(args))
+        self._last = target
+        if target is not self:
+            return target.solve_device(args, var_ptr, check)
         if not check:
             N.check(N.lib().cvq_solve(self._h, C.byref(args), C.c_void_p(var_ptr), None, N.MEM_DEVICE), "cvq_solve")
             return None
@@ -261,6 +286,8 @@ class QuadraturePlan:
         """Synchronise and check the last device-mode solve / finalize: raises NativeError
         (CVQ_ERR_NUMERIC) if a date did not converge within the bisection budget; returns
         the reference's bisection iteration count."""
+        if self._last is not None and self._last is not self:
+            return self._last.solve_status()
         it = C.c_int32(0)
         N.check(N.lib().cvq_solve_status(self._h, C.byref(it)), "cvq_solve_status")
         return int(it.value)
@@ -272,6 +299,10 @@ class QuadraturePlan:
         return int(s.value)
 
     def solve_local(self, args: N.CvqSolveArgs, header_ptr: int, snaps_ptr: int) -> None:
+        target = self._route(self._top(args))
+        self._last = None                        # the finalize (on this plan) reports the status
+        if target is not self:
+            return target.solve_local(args, header_ptr, snaps_ptr)
         N.check(N.lib().cvq_solve_local(self._h, C.byref(args), C.c_void_p(header_ptr), C.c_void_p(snaps_ptr)),
                 "cvq_solve_local")
 

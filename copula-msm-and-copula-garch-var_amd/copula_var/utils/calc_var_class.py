@@ -32,10 +32,36 @@ from ..data_loader.load_data import IndexReturnsRetriever
 from ..engine import QuadraturePlan
 
 
+DEVICE_MODELS = ("msm", "garch", "mean_reverting")
+DEVICE_COPULAS = ("student", "gaussian", "plackett")
+
+
+def check_device_adapter(method) -> None:
+    """The device evaluates the integrand itself (integrated_function is not a per-node
+    callback here), so an adapter must name a device model and copula: `model_kind` in
+    DEVICE_MODELS and `copula_kind` in DEVICE_COPULAS, as the factory's adapters do.  A
+    user-written VaRCalculationMethod without them fails here, before any in-sample work."""
+    model = getattr(method, "model_kind", None)
+    copula = getattr(method, "copula_kind", None)
+    bad = []
+    if model not in DEVICE_MODELS:
+        bad.append(f"model_kind={model!r} (one of {DEVICE_MODELS})")
+    if copula not in DEVICE_COPULAS:
+        bad.append(f"copula_kind={copula!r} (one of {DEVICE_COPULAS})")
+    if bad:
+        raise ValueError(
+            f"{type(method).__name__} cannot run on the device engine: it needs " + " and ".join(bad)
+            + ". The integrand is evaluated inside the HIP quadrature (cvq_slab / cvq_solve), so a "
+              "VaRCalculationMethod must be one of the factory's (copula x model) adapters or "
+              "declare those two attributes; a Python integrated_function is not called "
+              "(INTEGRATION.md, 'Plug-in adapters').")
+
+
 class ValueAtRiskCalcualtion:
     def __init__(self, tickers, start_date, in_sample_data_num, VaRCalculationMethod, end_date=None,
                  num_points=100, weights=np.array([0.5, 0.5]), *args, copula_params=None, device=0,
                  strategy="auto", **kwargs):
+        check_device_adapter(VaRCalculationMethod)
         self.num_points = num_points
         self.tickers = tickers
         self.start_date = start_date

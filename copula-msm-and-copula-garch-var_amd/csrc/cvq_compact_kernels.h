@@ -165,15 +165,27 @@ __device__ __forceinline__ double wave_incl_scan_f64(double v) {
     return v;
 }
 
+// The zeros of the tail cell's F (non-decreasing in v: node values >= 0, a NaN makes every later F
+// NaN) as the interval [vza, vzb) of mids, from F just above lo (Flo) and the thresholds of the first
+// tie-group end with F == 0 (za, +inf if none) and the first with !(F <= 0) (zb, +inf if none):
+// Flo > 0 or NaN: no zeros; Flo == 0: F is zero up to zb; Flo < 0 (the reference's first level can
+// leave F at the CDF minus a constant, Q1): F may pass through exactly 0 from za up to zb.
+__device__ __forceinline__ void zero_interval(double Flo, double za, double zb, double& vza, double& vzb) {
+    const double inf = __builtin_inf();
+    vza = (Flo == 0.0) ? -inf : (Flo < 0.0 ? za : inf);
+    vzb = zb;
+}
+
 // The remaining R = K - it bisection levels of a date in closed form (P.exact_walk: every bracket's
 // bisection points are exact dyadics, host-checked by dyadic_walk_ok).  Every decision is "mid >=
 // v_c" (hi = mid), so after R levels the bracket is the cell (lo + c wR, lo + (c + 1) wR] holding v_c
 // (kc 0: every mid decides high, c = 0; kc 1: none does, c = 2^R - 1), and level l's bracket is that
 // cell's ancestor c >> (R - l): mid_l = lo + (2 (c >> (R - l)) + 1) w 2^-(l+1), all exact.  The Q4
-// bit of level l is mid_l >= v_z (kz 0: always, 1: never).  Called by all 64 lanes of one wave
-// (lane l = level it + l); lo, hi, it, nt, mask come out identical in every lane.
-__device__ __forceinline__ void dyadic_walk(const SolveConst& P, int kc, double vcs, int kz, double vzs, double& lo,
-                                            double& hi, int& it, int& nt, uint64_t& mask, double* sn) {
+// bit of level l is "F(mid_l) != 0": F is non-decreasing, so its zeros are one v-interval and the
+// bit is !(v_za <= mid_l < v_zb) (zero_interval).  Called by all 64 lanes of one wave (lane l =
+// level it + l); lo, hi, it, nt, mask come out identical in every lane.
+__device__ __forceinline__ void dyadic_walk(const SolveConst& P, int kc, double vcs, double vza, double vzb,
+                                            double& lo, double& hi, int& it, int& nt, uint64_t& mask, double* sn) {
     const int lane = threadIdx.x & 63;
     const int R = P.K - it;                                    // 1 <= R <= 52
     const double w = hi - lo, wR = ldexp(w, -R), top = ldexp(1.0, R) - 1.0;
@@ -187,7 +199,7 @@ __device__ __forceinline__ void dyadic_walk(const SolveConst& P, int kc, double 
     const double cl = floor(ldexp(c, lane - R));
     const double mid = fma(2.0 * cl + 1.0, ldexp(w, -(lane + 1)), lo);
     if (act) sn[it + lane] = mid;
-    const unsigned long long bz = __ballot(act && (kz == 0 || (kz == 2 && mid >= vzs)));
+    const unsigned long long bz = __ballot(act && !(mid >= vza && mid < vzb));
     const unsigned long long bt = __ballot(act && !(ldexp(w, -lane) > P.tol));
     if (nt < 0 && bt) nt = it + (int)__builtin_ctzll(bt);
     mask |= bz << it;
@@ -912,27 +924,31 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             Stot += x;
         }
         const double Flo = ustack ? prev : prev - Stot;           // F just above lo
-        int mc = NPT, mz = NPT;                                   // first crossing / nonzero group end
+        // first crossing / first zero / first positive (or NaN) group end (zero_interval)
+        int mc = NPT, ma = NPT, mz = NPT;
 #pragma unroll
         for (int m = NPT - 1; m >= 0; --m) {
             if (!(wd[m] & kTlGroupEnd) || tid * NPT + m >= cnt) continue;
             const double pa = base + pre[m];
             const double Fv = ustack ? prev + pa : prev - (Stot - pa);
             if (!(Fv < P.obj)) mc = m;
-            if (Fv != 0.0) mz = m;
+            if (Fv == 0.0) ma = m;
+            if (!(Fv <= 0.0)) mz = m;
         }
         // first thread (lowest positions) holding each: wave ballots, then the block's waves
-        const unsigned long long bc = __ballot(mc < NPT), bz = __ballot(mz < NPT);
-        int* ew = (int*)(red + parity * (3 * (NT / 64)));         // the other reduction half: 2 ints / wave
+        const unsigned long long bc = __ballot(mc < NPT), ba = __ballot(ma < NPT), bz = __ballot(mz < NPT);
+        int* ew = (int*)(red + parity * (3 * (NT / 64)));         // the other reduction half: 3 ints / wave
         parity ^= 1;
         // the first flagged thread of the wave holds the wave's first crossing; its position goes
         // to LDS, and the walk compares each mid with that node's v* from the plan's sorted list
         // (measured faster than re-evaluating the membership test x_j <= (mid - x_r w1) / w0)
-        const int lc = bc ? (int)__builtin_ctzll(bc) : 0, lz = bz ? (int)__builtin_ctzll(bz) : 0;
-        const int mcl = __shfl(mc, lc, 64), mzl = __shfl(mz, lz, 64);
+        const int lc = bc ? (int)__builtin_ctzll(bc) : 0, la = ba ? (int)__builtin_ctzll(ba) : 0,
+                  lz = bz ? (int)__builtin_ctzll(bz) : 0;
+        const int mcl = __shfl(mc, lc, 64), mal = __shfl(ma, la, 64), mzl = __shfl(mz, lz, 64);
         if (lane == 0) {
             int* e = ew + 4 * (tid >> 6);
             e[0] = bc ? ((tid >> 6) * 64 + lc) * NPT + mcl : kNoPos;
+            e[1] = ba ? ((tid >> 6) * 64 + la) * NPT + mal : kNoPos;
             e[2] = bz ? ((tid >> 6) * 64 + lz) * NPT + mzl : kNoPos;
         }
         __syncthreads();
@@ -941,27 +957,31 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         // levels in closed form, lane l = level it + l; else lane 0 walks them one by one
         const bool exact = P.exact_walk != 0;
         if (exact ? tid < 64 : tid == leader) {
-            int ec = kNoPos, ez = kNoPos;
+            int ec = kNoPos, ea = kNoPos, ez = kNoPos;
 #pragma unroll
             for (int w = 0; w < NT / 64; ++w) {                   // waves in position order: first wins
                 const int* e = ew + 4 * w;
                 if (ec == kNoPos && e[0] != kNoPos) ec = e[0];
+                if (ea == kNoPos && e[1] != kNoPos) ea = e[1];
                 if (ez == kNoPos && e[2] != kNoPos) ez = e[2];
             }
             // kind: 0 = every mid (F just above lo already decides), 1 = no mid, 2 = mids at or
             // above the node's threshold (v* loaded from the plan's sorted list)
             const int kc = !(Flo < P.obj) ? 0 : (ec == kNoPos ? 1 : 2);
-            const int kz = (Flo != 0.0) ? 0 : (ez == kNoPos ? 1 : 2);
-            const double vcs = kc == 2 ? G.tvs[ps + ec] : 0.0, vzs = kz == 2 ? G.tvs[ps + ez] : 0.0;
+            const double vcs = kc == 2 ? G.tvs[ps + ec] : 0.0;
+            const double inf = __builtin_inf();
+            double vza, vzb;
+            zero_interval(Flo, (Flo < 0.0 && ea != kNoPos) ? G.tvs[ps + ea] : inf,
+                          (!(Flo > 0.0) && ez != kNoPos) ? G.tvs[ps + ez] : inf, vza, vzb);
             if (exact) {
-                dyadic_walk(P, kc, vcs, kz, vzs, lo, hi, it, nt, mask, sn);
+                dyadic_walk(P, kc, vcs, vza, vzb, lo, hi, it, nt, mask, sn);
             } else {
                 for (; it < P.K; ++it) {
                     const double mid = (lo + hi) / 2;
                     sn[it] = mid;
                     if (nt < 0 && !(hi - lo > P.tol)) nt = it;
                     const bool geq = kc == 0 || (kc == 2 && mid >= vcs);
-                    const bool nz = kz == 0 || (kz == 2 && mid >= vzs);
+                    const bool nz = !(mid >= vza && mid < vzb);
                     if (nz) mask |= (1ull << it);
                     ustack = !geq;
                     if (ustack) lo = mid; else hi = mid;

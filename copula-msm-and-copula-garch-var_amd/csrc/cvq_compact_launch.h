@@ -14,6 +14,8 @@
 #ifndef CVQ_COMPACT_NT
 #define CVQ_COMPACT_NT 256
 #endif
+// the block tail's list words hold a row and a column < compact_max_n() = 8 NT in 11-bit fields
+static_assert(8 * CVQ_COMPACT_NT - 1 <= (int)cvq::kTlRowMask, "tail list fields overflow");
 
 namespace cvq {
 

@@ -1316,7 +1316,9 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if (e == hipSuccess) e = hipMemcpy(p->d_svs, p->hvs.data(), nv * sizeof(double), hipMemcpyHostToDevice);
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     }
-    if (p->strategy == CVQ_STRATEGY_COMPACT) {         // exact level thresholds + grid lookup buckets
+    // exact level thresholds + grid lookup buckets; only for grids k_compact runs (larger ones solve
+    // on k_direct, and the tail list's 11-bit row / column fields would overflow)
+    if (p->strategy == CVQ_STRATEGY_COMPACT && n <= compact_max_n()) {
         std::vector<double> vs;
         build_vstar(p->hx, S.w0, S.w1, vs);
         p->hvc.clear();

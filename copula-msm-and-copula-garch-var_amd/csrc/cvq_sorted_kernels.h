@@ -931,8 +931,8 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 const double Flo = ustack ? prev : prev - Stot;   // F just above lo
                 const double nx = __shfl(tx[0], (lane + 1) & 63, 64);
                 double pa = incl - run;
-                int mc = TPL, mz = TPL;
-                double vc = 0.0, vz = 0.0;
+                const double inf = __builtin_inf();
+                double vc = inf, va = inf, vz = inf;        // first crossing / zero / positive-or-NaN end
 #pragma unroll
                 for (int m = 0; m < TPL; ++m) {
                     const bool in = tx[m] > lo && tx[m] <= hi;
@@ -940,15 +940,18 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                     const double tn = m + 1 < TPL ? tx[m + 1] : nx;
                     const bool gend = in && (lane * TPL + m == tot - 1 || !(tn <= tx[m]));   // last of its v*
                     const double Fv = ustack ? prev + pa : prev - (Stot - pa);
-                    if (gend && mc == TPL && !(Fv < P.obj)) { mc = m; vc = tx[m]; }
-                    if (gend && mz == TPL && Fv != 0.0) { mz = m; vz = tx[m]; }
+                    if (gend && vc == inf && !(Fv < P.obj)) vc = tx[m];
+                    if (gend && va == inf && Fv == 0.0) va = tx[m];
+                    if (gend && vz == inf && !(Fv <= 0.0)) vz = tx[m];
                 }
-                const unsigned long long bc = __ballot(mc < TPL), bz = __ballot(mz < TPL);
+                const unsigned long long bc = __ballot(vc != inf), ba = __ballot(va != inf), bz = __ballot(vz != inf);
                 const int kc = !(Flo < P.obj) ? 0 : (bc ? 2 : 1);
-                const int kz = (Flo != 0.0) ? 0 : (bz ? 2 : 1);
                 const double vcs = __shfl(vc, bc ? (int)__builtin_ctzll(bc) : 0, 64);
-                const double vzs = __shfl(vz, bz ? (int)__builtin_ctzll(bz) : 0, 64);
-                dyadic_walk(P, kc, vcs, kz, vzs, lo, hi, it, nt, mask, sn);
+                const double vas = ba ? __shfl(va, (int)__builtin_ctzll(ba), 64) : inf;
+                const double vzs = bz ? __shfl(vz, (int)__builtin_ctzll(bz), 64) : inf;
+                double vza, vzb;
+                zero_interval(Flo, vas, vzs, vza, vzb);
+                dyadic_walk(P, kc, vcs, vza, vzb, lo, hi, it, nt, mask, sn);
             }
         } else if (tid < 64) {
             double tx[TPL], ty[TPL];

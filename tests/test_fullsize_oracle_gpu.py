@@ -202,3 +202,66 @@ def test_slabs_ending_at_zero(case, strategy):
                                        atol=SLAB_ATOL, err_msg=f"{case} {strategy} {b}")
     finally:
         p.close()
+
+
+def test_auto_2d_grid_above_sorted_limit():
+    """A 2-D GARCH grid with num_points > 512 (SORTED's limit): 'auto' picks COMPACT, and the
+    solve matches the oracle (auto once chose SORTED there and every solve failed)."""
+    from copula_var import synthetic, tables
+    from oracle.quadrature import calc_var
+    c = synthetic.baseline_configs()[1].with_(T=8, num_points=600)
+    rets = synthetic.simulate_returns(c)
+    _, ptf, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
+    ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
+    p = _plan(c, ipt, uvs, ggp)
+    try:
+        assert p.strategy == "compact"
+        var, it = p.calc_var(ptf)
+    finally:
+        p.close()
+    P = _problem(c, ipt, uvs, ggp)
+    ref, ref_it, _ = calc_var(P.compute_integral, P.T, ptf)
+    assert it == ref_it
+    assert np.array_equal(var, ref)
+
+
+@pytest.mark.parametrize("case", ["cfg1", "cfg4_k4_n16"])
+def test_auto_routes_device_solves_above_v_cap(case):
+    """solve_device / solve_local on an 'auto' SORTED plan with a guess above v_cap = 0 route to
+    the unrestricted sibling, on the plan's stream (only the host entry points did)."""
+    import torch
+    from conftest import load_golden
+    from copula_var.engine import QuadraturePlan, solve_args
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden(case)
+    msm = str(z["model"]) == "msm"
+    vs = z.get("unique_vol_states")
+    per = (z["forecasts_by_states"], z["forecasts"]) if msm else z["sigma_forecasts"]
+    P = Problem(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+                z["combos"], z["weights"], z["copula_params"], per, vs)
+    ref, _, _ = calc_var(P.compute_integral, P.T, 0.0, first_guess=0.25)
+    p = QuadraturePlan(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
+                       z["combos"], z["weights"], z["copula_params"], vol_states=vs, strategy="auto")
+    s = torch.cuda.Stream()
+    try:
+        assert p.strategy == "sorted"
+        p.set_stream(s.cuda_stream)
+        p.set_dates(per if msm else [per])
+        args = solve_args(0.0, first_guess=0.25)
+        out = torch.empty(P.T, dtype=torch.float64, device="cuda")
+        with torch.cuda.stream(s):
+            p.solve_device(args, out.data_ptr())
+        p.solve_status()
+        s.synchronize()
+        assert p._wide is not None and p._wide._stream == s.cuda_stream
+        assert np.array_equal(out.cpu().numpy(), ref)
+        # the sharded entry points: local solve on the sibling, finalize on this plan
+        ln, hoff = QuadraturePlan.packed_block_len(args, P.T)
+        blk = torch.zeros(ln, dtype=torch.float64, device="cuda")
+        with torch.cuda.stream(s):
+            p.solve_local(args, blk[hoff:].data_ptr(), blk.data_ptr())
+            p.solve_finalize_packed(args, blk.data_ptr(), 1, P.T, P.T, out.data_ptr())
+        p.solve_status()
+        assert np.array_equal(out.cpu().numpy(), ref)
+    finally:
+        p.close()
