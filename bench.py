@@ -83,6 +83,9 @@ def parse():
                     help="1 GPU: also time end-to-end steps (device forecast tables + solve, from returns)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="independent batches in flight (one plan + HIP stream each); 1 = one batch at a time")
+    ap.add_argument("--nu", type=float, default=None,
+                    help="Student copula nu instead of the config's (e.g. 5.364, an IFM-fitted value: the "
+                         "non-integer node power path)")
     ap.add_argument("--time-all", type=int, default=0,
                     help="HIP-event time every kernel kind (adds event records to the timed region)")
     return ap.parse_args()
@@ -126,6 +129,10 @@ def main():
         else:
             dist.init_process_group("gloo")
     cfg = synthetic.baseline_configs()[a.config]
+    if a.nu is not None:
+        if cfg.copula != "student":
+            raise SystemExit(f"--nu applies to Student-copula configs; config {a.config} is {cfg.copula}")
+        cfg = cfg.with_(nu=float(a.nu))
     if a.strategy == "auto":
         a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points)
     strong = a.global_dates is not None
@@ -267,15 +274,25 @@ def main():
     fp64_tflops = flop_launch / dom_avg_s / 1e12 if dom_avg_s > 0 else 0.0
     alg_bytes = 8.0 * plan.reach_nodes * per          # one f64 joint-mass word per reachable node
     achieved_gbs = alg_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
-    traffic = None
+    # PMC HBM bytes per launch (profiles/pmc_traffic_cfg<N>.json, tools/pmc_summary.py): attached only
+    # when that pass measured THIS library build (sha of libcvq.so), the same strategy and launch size
+    traffic, traffic_src = None, "no PMC pass of this library build (tools/pmc.sh)"
+    lib_sha = _lib_sha16()
     pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_cfg{a.config}.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("dates_per_launch") == per and pm.get("strategy", "prefix") == a.strategy:
+            if (pm.get("lib_sha16") == lib_sha and pm.get("dates_per_launch") == per
+                    and pm.get("strategy") == a.strategy):
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = f"profiles/pmc_traffic_cfg{a.config}.json (FETCH_SIZE + WRITE_SIZE, lib {lib_sha})"
         except Exception:
             traffic = None
+    pmc_gbs = traffic / dom_avg_s / 1e9 if (traffic is not None and dom_avg_s > 0) else None
+    # the binding roofline: FP64 VALU unless the measured HBM traffic is the larger fraction of its
+    # peak (the algorithmic bytes of SURVEY §8d are notional -- the solve never materialises the mass)
+    fp64_frac = fp64_tflops / FP64_PEAK_TFLOPS
+    hbm_bound = pmc_gbs is not None and pmc_gbs / HBM_PEAK_GBS > fp64_frac
     kernels = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt.items() if v[1]}
     kernels_single = {k: {"avg_us": (v[0] / max(v[1], 1)) * 1e3, "launches": v[1]} for k, v in kt1.items() if v[1]}
 
@@ -306,13 +323,18 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic ({c.model} returns, seed {c.seed}; injected in-sample params; fixed copula)",
-            "config": {"workload": f"cfg{a.config}: {c.name}", "model": c.model, "copula": c.copula,
+            "config": {"workload": f"cfg{a.config}: {c.name}" + (f", nu {c.nu}" if a.nu is not None else ""),
+                       "model": c.model, "copula": c.copula,
                        "dim": c.dim, "grid": f"{c.num_points}^{c.dim}", "dates_per_gpu": per,
                        "global_dates": T_total, "n_in": c.n_in, "parallelism": f"dates/dp{world}",
                        "strategy": a.strategy, "inflight": nf},
             "single_solve": single,
-            "roofline": {"bound": "fp64-valu", "achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": fp64_tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kname,
+            "roofline": {"bound": "hbm" if hbm_bound else "fp64-valu",
+                         "achieved": pmc_gbs if hbm_bound else fp64_tflops,
+                         "peak": HBM_PEAK_GBS if hbm_bound else FP64_PEAK_TFLOPS,
+                         "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                         "frac": pmc_gbs / HBM_PEAK_GBS if hbm_bound else fp64_frac,
+                         "traffic": traffic, "traffic_source": traffic_src, "lib_sha16": lib_sha, "kernel": kname,
                          "flop_per_node": flop_node,
                          "flop_basis": "nodes evaluated (device count)" if nodes_eval is not None
                                        else "reachable nodes",
@@ -325,9 +347,14 @@ def main():
                          "reach_basis": {"flop_per_launch": flop_reach,
                                          "frac": flop_reach / dom_avg_s / 1e12 / FP64_PEAK_TFLOPS
                                          if dom_avg_s > 0 else 0.0},
-                         "hbm": {"alg_bytes_per_launch": alg_bytes, "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
-                                 "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                                 "pmc_bytes_per_launch": traffic}},
+                         "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": fp64_frac},
+                         "hbm": {"pmc_bytes_per_launch": traffic, "pmc_achieved": pmc_gbs,
+                                 "pmc_frac": pmc_gbs / HBM_PEAK_GBS if pmc_gbs is not None else None,
+                                 "alg_bytes_per_launch": alg_bytes, "alg_achieved": achieved_gbs,
+                                 "alg_frac": achieved_gbs / HBM_PEAK_GBS, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "note": "alg_*: 8 B x reachable nodes (SURVEY §8d), notional -- the solve never "
+                                         "writes the joint mass; pmc_*: measured FETCH_SIZE + WRITE_SIZE"}},
             "kernels": kernels,
             "kernels_single": kernels_single,
             "forecast_stage_s": t_fc,
@@ -409,6 +436,17 @@ def cpu_baseline(c, ipt, uvs, ggp, ptf_mean, gpu_var, a):
             "sample": f"first {S} dates of the same workload, full calc_var control flow "
                       f"({it} bisection iterations), joblib n_jobs={jobs}, scalar t.ppf; wall {wall:.1f}s",
             "cpu": _cpu_model()}
+
+
+def _lib_sha16():
+    """Build id of the loaded HIP library: the first 16 hex digits of sha256(libcvq.so)."""
+    import hashlib
+    from copula_var import _native
+    h = hashlib.sha256()
+    with open(_native.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
 
 
 def _cpu_model():

@@ -29,6 +29,7 @@ def solve_args(ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_gue
                           float(min_var), float(max_var), float(lower), float(tolerance), float(ptf_mean))
 
 
+MAX_N = 512                           # num_points limit of every plan (cvq_plan_create)
 SORTED_MAX_N = {2: 512, 3: 255}      # sorted_max_n (cvq_sorted_kernels.h)
 PREFIX_MAX_N_3D = 64                  # PREFIX solves at most 4096 rows (cvq_plan.hip pick_solve_shape)
 MATERIALISED = ("prefix", "sorted", "sweep")   # strategies that hold only nodes with level <= v_cap
@@ -39,14 +40,15 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None) -> str:
     among those that run it: COMPACT for 2-asset MSM (cfg 2: 20.3M vs SORTED 16.4M
     VaR-dates/s), SORTED for 2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for
     3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
-    bounds the choice: 2-D SORTED takes n <= 512 (larger 2-D grids go to COMPACT, which
-    hands n > 2048 to k_direct), 3-D SORTED n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
+    bounds the choice: every 2-D strategy takes n <= 512 (the plan's limit, so a 2-D
+    rule never picks a strategy that fails later), 3-D SORTED n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
     takes n > 255.  SORTED and PREFIX hold the nodes with level <= v_cap only;
     QuadraturePlan(strategy="auto") routes a query above v_cap to an unrestricted
     sibling plan (COMPACT / DIRECT in 2-D, SORTED with v_cap at the grid's top in 3-D)."""
     if dim == 2:
-        # SORTED holds 2-D grids up to SORTED_MAX_N[2]; COMPACT runs larger ones (k_direct past 2048)
-        return "compact" if model == "msm" or (n is not None and n > SORTED_MAX_N[2]) else "sorted"
+        if n is not None and n > MAX_N:
+            raise ValueError(f"num_points <= {MAX_N} (every strategy: cvq_plan_create), got {n}")
+        return "compact" if model == "msm" else "sorted"
     if n is None or n <= SORTED_MAX_N[3]:
         return "sorted"
     raise ValueError(f"3-asset grids support num_points <= {SORTED_MAX_N[3]} (SORTED), got {n}")

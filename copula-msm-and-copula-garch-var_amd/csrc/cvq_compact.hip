@@ -7,7 +7,7 @@
 
 namespace cvq {
 
-int compact_max_n() { return 8 * CVQ_COMPACT_NT; }
+int compact_max_n() { return 2 * CVQ_COMPACT_NT; }      // 1 or 2 rows per thread (launch_f)
 int compact_tail_cap() { return CVQ_COMPACT_NT * kBlkPerThread; }   // block tail: cell nodes per workgroup
 
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,

@@ -14,8 +14,8 @@
 #ifndef CVQ_COMPACT_NT
 #define CVQ_COMPACT_NT 256
 #endif
-// the block tail's list words hold a row and a column < compact_max_n() = 8 NT in 11-bit fields
-static_assert(8 * CVQ_COMPACT_NT - 1 <= (int)cvq::kTlRowMask, "tail list fields overflow");
+// the block tail's list words hold a row and a column < compact_max_n() = 2 NT in 11-bit fields
+static_assert(2 * CVQ_COMPACT_NT - 1 <= (int)cvq::kTlRowMask, "tail list fields overflow");
 
 namespace cvq {
 
@@ -50,7 +50,7 @@ void launch_r(const CompactLaunch& L) {
                        dim3(NT), lds_gen, L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.defer, L.T);
 }
 
-// rows per thread: ceil(n / NT) rounded up to 1, 2, 4 or 8 (n <= 8 NT)
+// rows per thread: 1 or 2 (n <= compact_max_n() = 2 NT, the plan's num_points limit of 512)
 template <int COP, bool MSM, int PM, bool FUSED>
 void launch_f(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
@@ -60,9 +60,7 @@ void launch_f(const CompactLaunch& L) {
     launch_r<COP, MSM, PM, FUSED, 1>(L);
 #else
     if (rpt <= 1) launch_r<COP, MSM, PM, FUSED, 1>(L);
-    else if (rpt <= 2) launch_r<COP, MSM, PM, FUSED, 2>(L);
-    else if (rpt <= 4) launch_r<COP, MSM, PM, FUSED, 4>(L);
-    else launch_r<COP, MSM, PM, FUSED, 8>(L);
+    else launch_r<COP, MSM, PM, FUSED, 2>(L);
 #endif
 }
 

@@ -2,87 +2,46 @@
 // its template instances compile in parallel with cvq_plan.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #define CVQ_NO_PLAN_KERNELS
 
-#include "cvq_common.h"
-#include "cvq_sorted_kernels.h"
+#include "cvq_sorted_launch.h"
 
 namespace cvq {
 namespace {
 
-
-struct SortedLaunch {
-    const StaticDev& S;
-    const SolveConst& P;
-    const SortedGeom& G;
-    long long T;
-    hipStream_t stream;
-    const double *a, *tA, *tB, *pi;
-    int mode;
-    const double* bounds;
-    double *out, *snaps;
-    Header* hdr;
-    bool fused;
-    double* stamps;
-    bool sweep;
-};
-
-template <int COP, bool MSM, int DIM, int PM, bool FUSED, int LAY>
-void launch_l(const SortedLaunch& L) {
-    if constexpr (DIM == 2) {
-        if (L.sweep && L.mode == 0) {                  // SWEEP: one pass per cell (2-D solves)
-            hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY, true>), dim3((unsigned)L.T),
-                               dim3(kSortNT), sorted_lds_bytes(L.S.n, kSortNT, DIM, true, LAY), L.stream, L.S, L.P,
-                               L.G, L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
-            return;
-        }
+// Compute units of a device (cached; MI355X: 256).
+int device_cus() {
+    static int cus[64] = {0};
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+    if (!cus[d]) {
+        int v = 0;
+        cus[d] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0) ? v : 256;
     }
-    hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, kSortNT, PM, FUSED, LAY>), dim3((unsigned)L.T), dim3(kSortNT),
-                       sorted_lds_bytes(L.S.n, kSortNT, DIM, false, LAY), L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB,
-                       L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
-}
-
-template <int COP, bool MSM, int DIM, int PM, bool FUSED>
-void launch_f(const SortedLaunch& L) {
-    if constexpr (DIM == 2) {
-        if constexpr (COP == CVQ_STUDENT && PM > 0) {
-            if (L.G.layout == kLay2W) { launch_l<COP, MSM, DIM, PM, FUSED, kLay2W>(L); return; }
-        }
-        launch_l<COP, MSM, DIM, PM, FUSED, kLay2>(L);
-    } else {
-        if (sorted_layout(DIM, L.S.n) == kLay3F) launch_l<COP, MSM, DIM, PM, FUSED, kLay3F>(L);
-        else launch_l<COP, MSM, DIM, PM, FUSED, kLay3G>(L);
-    }
-}
-
-template <int COP, bool MSM, int DIM, int PM>
-void launch_pm(const SortedLaunch& L) {
-    if (L.fused) launch_f<COP, MSM, DIM, PM, true>(L);
-    else launch_f<COP, MSM, DIM, PM, false>(L);
-}
-
-template <int COP, bool MSM, int DIM>
-void launch_d(const SortedLaunch& L) {
-    if constexpr (COP == CVQ_STUDENT) {
-        // integer nu + dim: b^-(nu+dim)/2 by squarings and one rcp (nu = 6: 8 in 2-D, 9 in 3-D)
-        if (L.S.node_m == DIM + 6) { launch_pm<COP, MSM, DIM, DIM + 6>(L); return; }
-    }
-    launch_pm<COP, MSM, DIM, 0>(L);
-}
-
-template <int COP, bool MSM>
-void launch_m(const SortedLaunch& L) {
-    if (L.S.dim == 2) launch_d<COP, MSM, 2>(L);
-    else if constexpr (COP != CVQ_PLACKETT) launch_d<COP, MSM, 3>(L);
-}
-
-template <int COP>
-void launch_c(const SortedLaunch& L) {
-    if (L.S.model == CVQ_MSM) launch_m<COP, true>(L);
-    else launch_m<COP, false>(L);
+    return cus[d];
 }
 
 }  // namespace
+
+// Threads per date (one workgroup each).  A date is a chain of dependent phases (tables, two
+// fixed slabs, ~10 reduced levels, the tail), so a launch with few dates per CU is latency
+// bound: wider workgroups split every range sum over more lanes and shorten the chain.  The
+// widest width whose waves the chip holds at once (T NT / 64 <= CUs x 4 SIMDs x the 2-D
+// kernel's 5 waves per SIMD; 3-D: 4) -- i.e. a strong-scaling block of a few hundred dates per
+// GPU runs 1024- or 512-thread dates, a full batch 256.  CVQ_SORT_NT (256 / 512 / 1024)
+// overrides (A/B).
+int sorted_threads(long long T, int dim, bool narrow) {
+    const char* ev = getenv("CVQ_SORT_NT");            // read per launch: tests switch it per case
+    const int env = ev ? atoi(ev) : 0;
+    if (narrow) return kSortNT;
+    if (env == 256 || env == 512 || env == 1024) return env;
+    const long long waves = (long long)device_cus() * 4 * sorted_min_waves(dim);
+    for (int nt = 1024; nt > kSortNT; nt >>= 1)
+        if (T * (nt / 64) <= waves) return nt;
+    return kSortNT;
+}
 
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
                   const double* a, const double* tA, const double* tB, const double* pi, bool fused, int mode,
@@ -92,10 +51,14 @@ int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, 
                 "libcvq objects built from different headers (rebuild all)");
     CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
     const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
-    switch (S.copula) {
-        case CVQ_GAUSSIAN: launch_c<CVQ_GAUSSIAN>(L); break;
-        case CVQ_STUDENT: launch_c<CVQ_STUDENT>(L); break;
-        default: launch_c<CVQ_PLACKETT>(L); break;
+    // SWEEP solves and the folded SWEEP records (kLay2W) exist at 256 threads only
+    CVQ_REQUIRE(mode < 2 || (G.pre && G.split_c >= 1 && G.layout != kLay2W && !sweep), CVQ_ERR_STATE,
+                "SPLIT pre-pass without its scratch");
+    const int nt = mode >= 2 ? kSortNT : sorted_threads(T, S.dim, (sweep && mode == 0) || G.layout == kLay2W);
+    switch (nt) {
+        case 1024: sorted_slice_1024(L); break;
+        case 512: sorted_slice_512(L); break;
+        default: sorted_launch_nt<kSortNT>(L); break;
     }
     CVQ_HIP_CHECK(hipGetLastError());
     return CVQ_OK;

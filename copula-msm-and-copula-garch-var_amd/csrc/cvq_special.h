@@ -386,8 +386,54 @@ __device__ __forceinline__ double fast_rcp(double r) {
     return y;
 }
 
+// exp(x): 2^k e^r, |r| <= ln2 / 2, degree-9 polynomial fitted to exp's relative error on that
+// interval (max 1.4e-14; the solve's decisions are unchanged by 1e-8 node noise).
+// For finite |x| < 1e9; x < -1075 underflows to 0, NaN stays NaN.
+__device__ __forceinline__ double exp_node(double x) {
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, x);      // ln2 hi (exact k * hi for |k| < 2^20)
+    r = fma(-k, 1.90821492927058770002e-10, r);             // ln2 lo
+    double p = 2.747468209548047e-06;
+    p = fma(p, r, 2.488396512173419e-05);
+    p = fma(p, r, 0.00019841616545137992);
+    p = fma(p, r, 0.001388880293639777);
+    p = fma(p, r, 0.008333332984833044);
+    p = fma(p, r, 0.041666667031658604);
+    p = fma(p, r, 0.1666666666788623);
+    p = fma(p, r, 0.499999999994599);
+    p = fma(p, r, 0.9999999999998875);
+    p = fma(p, r, 1.0000000000000127);
+    return __builtin_amdgcn_ldexp(p, (int)k);
+}
+
+// log(b) for finite b >= 1 (the node power's base): b = 2^k m, m in [sqrt(1/2), sqrt(2)),
+// log(1 + f) from s = f / (2 + f) and the published fdlibm e_log.c minimax polynomial in s^2
+// (< 1 ulp there; the reciprocal here is v_rcp_f64 + two Newton steps, ~1 ulp more), no
+// branches or library calls.
+__device__ __forceinline__ double log_node(double b) {
+    double m = __builtin_amdgcn_frexp_mant(b);             // [1/2, 1)
+    int k = __builtin_amdgcn_frexp_exp(b);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m + m : m;
+    k = lo ? k - 1 : k;
+    const double f = m - 1.0;
+    const double s = f * fast_rcp(2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                     2.857142874366239149e-01), 6.666666666666735130e-01);
+    const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
+#ifndef CVQ_POW_LIB
+#define CVQ_POW_LIB 0
+#endif
 // b^ex for b >= 1 with ex = -m/2 (m = node_m >= 0): squarings + one reciprocal;
-// m < 0 selects the general exp(ex * log b).  Used once per quadrature node.
+// m < 0 (non-integer nu: an IFM-fitted copula) selects exp(ex log b) from log_node / exp_node
+// (~1e-14 relative; the OCML pair cost ~210 instructions per node in the solve kernels' node
+// loops, ~10x the integer-nu node); b = inf -> 0 and NaN -> NaN, as pow gives them.
+// Used once per quadrature node.
 __device__ __forceinline__ double pow_node(double b, int m, double ex) {
     if (m >= 0) {
         double r = 1.0, s = b;
@@ -397,7 +443,9 @@ __device__ __forceinline__ double pow_node(double b, int m, double ex) {
         if (!(r < 1.0e300)) return r == r ? 0.0 : r;     // overflow -> 0, NaN stays NaN
         return fast_rcp(r);
     }
-    return exp(ex * log(b));
+    if (CVQ_POW_LIB) return exp(ex * log(b));
+    const double y = exp_node(ex * log_node(b));
+    return (b < 1.0e300) ? y : (b == b ? 0.0 : b);          // b^ex, ex <= -1/2: +inf -> 0, NaN stays NaN
 }
 
 // b^(-m/2) for b >= 1, general m >= 0 (m < 0: exp(ex log b)); no loop for m <= 16.

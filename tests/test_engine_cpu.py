@@ -10,8 +10,8 @@ def test_auto_strategy_rules():
     for m in ("garch", "mean_reverting"):
         assert auto_strategy(m, 2, 64) == "sorted"
         assert auto_strategy(m, 2, 512) == "sorted"
-        assert auto_strategy(m, 2, 513) == "compact"        # above SORTED's 2-D limit
-        assert auto_strategy(m, 2, 4096) == "compact"       # COMPACT hands n > 2048 to k_direct
+        with pytest.raises(ValueError, match="512"):
+            auto_strategy(m, 2, 513)                        # no plan takes n > 512: fail at the rule
     assert auto_strategy("msm", 3, 128) == "sorted"
     assert auto_strategy("garch", 3, 255) == "sorted"
     assert auto_strategy("msm", 2) == "compact"            # n unknown: the 2-D rule

@@ -35,9 +35,9 @@ def _need_gpu(gpu_available):
         pytest.fail("GPU tests were selected but no HIP device / libcvq.so is available")
 
 
-def _workload(cfg_no, T):
+def _workload(cfg_no, T, **kw):
     from copula_var import synthetic, tables
-    c = synthetic.baseline_configs()[cfg_no].with_(T=T)
+    c = synthetic.baseline_configs()[cfg_no].with_(T=T, **kw)
     rets = synthetic.simulate_returns(c)
     _, ptf_mean, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
     if c.model == "msm":
@@ -204,25 +204,17 @@ def test_slabs_ending_at_zero(case, strategy):
         p.close()
 
 
-def test_auto_2d_grid_above_sorted_limit():
-    """A 2-D GARCH grid with num_points > 512 (SORTED's limit): 'auto' picks COMPACT, and the
-    solve matches the oracle (auto once chose SORTED there and every solve failed)."""
+@pytest.mark.parametrize("strategy", ["auto", "compact", "sorted", "direct", "prefix"])
+def test_2d_grid_above_512_refused_at_creation(strategy):
+    """num_points > 512 is refused when the plan is created, for every strategy (ADVICE r03
+    feared an 'auto' plan that builds and then fails every solve)."""
     from copula_var import synthetic, tables
-    from oracle.quadrature import calc_var
-    c = synthetic.baseline_configs()[1].with_(T=8, num_points=600)
+    c = synthetic.baseline_configs()[1].with_(T=4, num_points=600)
     rets = synthetic.simulate_returns(c)
     _, ptf, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
     ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
-    p = _plan(c, ipt, uvs, ggp)
-    try:
-        assert p.strategy == "compact"
-        var, it = p.calc_var(ptf)
-    finally:
-        p.close()
-    P = _problem(c, ipt, uvs, ggp)
-    ref, ref_it, _ = calc_var(P.compute_integral, P.T, ptf)
-    assert it == ref_it
-    assert np.array_equal(var, ref)
+    with pytest.raises(ValueError, match="512"):
+        _plan(c, ipt, uvs, ggp, strategy=strategy)
 
 
 @pytest.mark.parametrize("case", ["cfg1", "cfg4_k4_n16"])
@@ -265,3 +257,36 @@ def test_auto_routes_device_solves_above_v_cap(case):
         assert np.array_equal(out.cpu().numpy(), ref)
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("strategy", ["auto", "compact", "sorted"])
+@pytest.mark.parametrize("cfg,T,S", [(2, 1000, 4), (5, 5000, 4)])
+def test_fitted_nu_full_size_matches_oracle(cfg, T, S, strategy):
+    """A fitted (non-integer) Student nu -- 5.364, SURVEY.md's measured scipy case -- takes the
+    general node power b^-(nu+2)/2 = exp(ex log b) (cvq_special.h pow_node: log_node /
+    exp_node) and the general t.ppf tables: full-size cfg 2 / cfg 5 workloads, S dates spread
+    over the VaR range against the oracle (VaR bit-identical, same bisection count), and the
+    whole batch free of NaN."""
+    from oracle.quadrature import calc_var
+    c, ipt, uvs, ggp, ptf = _workload(cfg, T, nu=5.364)
+    p = _plan(c, ipt, uvs, ggp, strategy=strategy)
+    try:
+        full, _ = p.calc_var(ptf)
+    finally:
+        p.close()
+    assert not np.isnan(full).any()
+    order = np.argsort(full, kind="stable")
+    idx = np.sort(order[np.linspace(0, T - 1, S).round().astype(int)])
+    sub = _subset(c, ipt, idx)
+    P = _problem(c, sub, uvs, ggp)
+    ref, ref_it, _ = calc_var(P.compute_integral, P.T, ptf)
+    p = _plan(c, sub, uvs, ggp, strategy=strategy)
+    try:
+        var, it = p.calc_var(ptf)
+        bounds = np.tile([-3.0, -2.0], (P.T, 1))
+        np.testing.assert_allclose(p.compute_integral(bounds), P.compute_integral(bounds), rtol=SLAB_RTOL,
+                                   atol=SLAB_ATOL)
+    finally:
+        p.close()
+    assert it == ref_it, (it, ref_it)
+    assert np.array_equal(var, ref), (cfg, strategy, float(np.max(np.abs(var - ref))))

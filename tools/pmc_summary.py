@@ -44,7 +44,12 @@ if mass:
     d = summ[mass[0]]
     fetch = d.get("FETCH_SIZE", 0.0) * 1024 * 2
     write = d.get("WRITE_SIZE", 0.0) * 1024
-    rec = {"kernel": mass[0], "config": cfg, "dates_per_launch": dates, "strategy": strategy,
+    import hashlib
+    root = os.environ.get("GRAFT_REPO_ROOT", ".")
+    lib = os.environ.get("CVQ_LIB") or os.path.join(root, "copula-msm-and-copula-garch-var_amd", "copula_var", "libcvq.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    rec = {"kernel": mass[0], "config": cfg, "dates_per_launch": dates, "strategy": strategy, "lib_sha16": sha,
+           "launches_averaged": len(vals[mass[0]].get("FETCH_SIZE", [])),
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "note": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide streaming reads); KiB -> bytes; "

@@ -16,7 +16,10 @@ scan() {   # config, dates...
   done
 }
 EXTRA=("$@")
-scan 3 5000 2500 1250 625
-scan 5 5000 2500 1250 625
-scan 4 2000 1000 500 250
-scan 2 1000 500 250 125
+for c in ${SCAN_CFGS:-3 5 4 2}; do
+  case $c in
+    3|5) scan $c 5000 2500 1250 625 ;;
+    4) scan 4 2000 1000 500 250 ;;
+    2) scan 2 1000 500 250 125 ;;
+  esac
+done
