@@ -119,6 +119,14 @@ def lib() -> C.CDLL:
             raise RuntimeError(
                 f"libcvq.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "or `make -C copula-msm-and-copula-garch-var_amd`; the VaR engine has no CPU fallback")
+        # One HIP runtime per process: torch (the device buffers, streams and RCCL around this
+        # library) ships its own libamdhip64.  Loaded after libcvq's (/opt/rocm), torch finds no
+        # GPU ("No HIP GPUs are available"); loaded first, libcvq binds to it.  So import torch
+        # before the library when it is installed.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = C.CDLL(LIB_PATH)
         _declare(_lib)
     return _lib

@@ -174,8 +174,6 @@ struct cvq_plan {
     std::vector<double> hvs;
     uint32_t* d_sidx = nullptr;  // [G]
     double* d_svs = nullptr;     // [G]
-    double* d_pre = nullptr;     // SPLIT pre-pass chunk sums [T][C][3 + 2^D]
-    size_t cap_pre = 0;
     int* d_tree = nullptr;       // [4][1 << tree_depth]
     int tree_depth = 0;
     int* d_sweep0 = nullptr;     // SWEEP: pass-0 boundary list
@@ -859,30 +857,6 @@ SortedGeom sorted_geom(const cvq_plan* p, bool solve) {
     return G;
 }
 
-// SPLIT (SORTED solves of small date blocks): chunks per date, or 0 for the one-kernel solve.  A
-// date's solve is a chain of dependent phases; with a few dates per CU (a strong-scaling block:
-// 625 of cfg 3 / 5's 5000 dates per GPU) the fixed slabs and the bracket's first levels set the
-// time, so two pre-passes spread them over C workgroups per date.  CVQ_SPLIT
-// (0 / 1) forces it off / on, CVQ_SPLIT_C and CVQ_SPLIT_D set C and the levels resolved from the
-// pre-pass (read per launch: tests switch them per case).
-constexpr int kSplitDatesPerCu = 0;                    // default: off until measured (set below)
-int split_chunks(const cvq_plan* p, int* depth) {
-    if (p->strategy != CVQ_STRATEGY_SORTED || p->layout == kLay2W) return 0;
-    const int* f = p->fixpos;
-    if (!(f[0] <= f[1] && f[1] <= f[2] && f[2] <= f[3])) return 0;   // pass 1 cuts (lower, sg1] at sg0, fg
-    const char* ev = getenv("CVQ_SPLIT");
-    const int force = ev ? atoi(ev) : -1;
-    if (force == 0) return 0;
-    int cus = 256, dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (force < 0 && p->T > (long long)kSplitDatesPerCu * cus) return 0;    // a full batch: one kernel
-    const char* ec = getenv("CVQ_SPLIT_C");
-    const char* ed = getenv("CVQ_SPLIT_D");
-    int C = ec ? atoi(ec) : (int)std::min<long long>(8, std::max<long long>(2, (5LL * cus + p->T - 1) / p->T));
-    *depth = std::min(std::max(ed ? atoi(ed) : 4, 0), kSplitMaxD);
-    return std::min(std::max(C, 1), 64);
-}
-
 int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
     if (sorted_family(p)) {
@@ -892,28 +866,10 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         const bool dbg_stamps = env_stamps || p->count_nodes;
         if (dbg_stamps && (rc = ensure_stamps(p))) return rc;
         p->nodes_valid = p->count_nodes;
-        SortedGeom G = sorted_geom(p, true);
-        const size_t abi = kernel_abi_key() ^ (sizeof(SortedGeom) << 40);
-        int D = 0;
-        const int C = split_chunks(p, &D);
-        if (C > 0) {                                   // pass 1, pass 2, then the solve reading their sums
-            const size_t need = (size_t)p->T * C * split_width(D);
-            if (p->cap_pre < need) {
-                if ((rc = dev_alloc(&p->d_pre, need))) return rc;
-                p->cap_pre = need;
-            }
-            G.pre = p->d_pre;
-            G.split_c = C;
-            G.split_d = D;
-            for (int mode = 2; mode <= 3; ++mode)
-                if ((rc = launch_sorted(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
-                                        direct_fused(p), mode, nullptr, nullptr, snaps, hdr, nullptr, false, abi)))
-                    return rc;
-        }
-        return launch_sorted(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
+        return launch_sorted(p->S, P, sorted_geom(p, true), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
                              direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
                              dbg_stamps ? (double*)p->d_stamps : nullptr,
-                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok, abi);
+                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok, kernel_abi_key() ^ (sizeof(SortedGeom) << 40));
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
@@ -1413,7 +1369,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
                     (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
-                    (void*)p->d_pidx, (void*)p->d_pvs, (void*)p->d_pre})
+                    (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;

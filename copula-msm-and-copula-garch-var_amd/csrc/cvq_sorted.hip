@@ -52,9 +52,7 @@ int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, 
     CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
     const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
     // SWEEP solves and the folded SWEEP records (kLay2W) exist at 256 threads only
-    CVQ_REQUIRE(mode < 2 || (G.pre && G.split_c >= 1 && G.layout != kLay2W && !sweep), CVQ_ERR_STATE,
-                "SPLIT pre-pass without its scratch");
-    const int nt = mode >= 2 ? kSortNT : sorted_threads(T, S.dim, (sweep && mode == 0) || G.layout == kLay2W);
+    const int nt = sorted_threads(T, S.dim, (sweep && mode == 0) || G.layout == kLay2W);
     switch (nt) {
         case 1024: sorted_slice_1024(L); break;
         case 512: sorted_slice_512(L); break;

@@ -89,21 +89,7 @@ struct SortedGeom {
     // between slab ends; the tail's prefix scan needs the tail cell's nodes in v* order)
     const uint32_t* tidx;
     const double* tvs;
-    // SPLIT (small date blocks): two pre-passes of split_c workgroups per date
-    // sum chunks of the fixed slabs' range and of the date's bracket; the solve adds the
-    // chunks in a fixed order.  pre: [T][split_c][3 + 2^split_d] (nullptr: no split)
-    double* pre;
-    int split_c;           // chunks (workgroups) per date
-    int split_d;           // bracket levels resolved from the pass-2 cell sums (<= kSplitMaxD)
 };
-constexpr int kSplitMaxD = 5;                          // <= 32 cells per bracket
-__host__ __device__ constexpr int split_width(int d) { return 3 + (1 << d); }   // doubles per (date, chunk)
-// chunk c of positions [ps, pe) split into C near-equal pieces
-__host__ __device__ inline void split_chunk(int ps, int pe, int C, int c, int* cs, int* ce) {
-    const int L = (pe - ps + C - 1) / C;
-    *cs = min(ps + c * L, pe);
-    *ce = min(*cs + L, pe);
-}
 
 // chunk geometry of a sweep over sorted positions [ps, pe): thread t takes [a0 + t L, a0 + (t + 1) L)
 __host__ __device__ inline void sweep_chunks(int ps, int pe, int nt, int* a0, int* L) {
@@ -257,10 +243,7 @@ __host__ __device__ constexpr int sorted_min_waves(int dim) {
 // prefix sums, and every thread then walks the subtree's levels from LDS (slab = difference of
 // two prefixes) with no further barrier.  Pass 0 covers (lower, sg1], so r0, the second slab
 // and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes one more.
-// PRE: the SPLIT pre-pass instance (mode 2: chunk sums of the fixed slabs' range (lower, sg1]
-// cut at sg0 and fg; mode 3: chunk sums of the date's bracket per cell of its depth-split_d
-// subtree), one workgroup per (date, chunk).
-template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false, bool PRE = false>
+template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false>
 __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
@@ -270,7 +253,7 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     constexpr int TPL = sorted_tail_per_lane(DIM), TCAP = sorted_tail_cap(DIM);
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
     const int ns = (n + 1) & ~1;                   // sorted_stride(n)
-    const long long t = PRE ? blockIdx.x / G.split_c : blockIdx.x;   // PRE: workgroup (date, chunk)
+    const long long t = blockIdx.x;
     // One LDS region holds EITHER the generic tables (reference semantics: z, B, w per
     // axis; axis 0 of 3-D: w = the i1 == 0 weight) OR the fast records (16 B per axis
     // entry; 3-D axis 0 twice, [n, 2n) = the plane i1 == 0), chosen per date.
@@ -773,54 +756,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         prevU = mid;
         return ustack;
     };
-    // ---- SPLIT: this date's chunk sums from the pre-passes, added in chunk order
-    const int SW = split_width(G.split_d);
-    const double* pre_t = G.pre ? G.pre + (size_t)t * G.split_c * SW : nullptr;
-    auto pre_sum = [&](int k) {
-        double v = 0.0;
-        for (int c = 0; c < G.split_c; ++c) v += pre_t[(size_t)c * SW + k];
-        return v;
-    };
-    // r0 = I(lower, fg], the second slab and the bracket from pass 1's sums (lower, sg0],
-    // (sg0, fg], (fg, sg1] (calc_var_class.py:114-149)
-    auto split_bracket = [&]() {
-        const double sA = pre_sum(0), sB = pre_sum(1), sC = pre_sum(2);
-        const double r0 = sA + sB;
-        const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-        const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
-        bracket(r0, nl, nu, (nl == P.fg) ? sC : sB);
-    };
-    // in-order boundary k (0 < k < 2^D) of the bracket's depth-D subtree: ub() of its heap node's mid
-    auto split_bound = [&](int k, int D) {
-        const int z = __builtin_ctz(k), l = D - 1 - z;
-        return tr[(1 << l) + (k >> (z + 1))];
-    };
-    if constexpr (PRE) {
-        const int c = (int)(blockIdx.x % G.split_c);
-        double* out = G.pre + ((size_t)t * G.split_c + c) * SW;
-        if (mode == 2) {                                   // pass 1: (lower, sg1] cut at sg0, fg
-            int cs, ce;
-            split_chunk(G.fix[0], max(G.fix[3], G.fix[0]), G.split_c, c, &cs, &ce);
-            const int b1 = min(max(G.fix[1], cs), ce), b2 = min(max(G.fix[2], b1), ce);
-            const double sA = team_sum(range_sum(cs, b1));
-            const double sB = team_sum(range_sum(b1, b2));
-            const double sC = team_sum(range_sum(b2, ce));
-            if (tid == 0) { out[0] = sA; out[1] = sB; out[2] = sC; }
-            return;
-        }
-        // pass 2: the bracket (from pass 1's sums) per cell of its depth-D subtree
-        split_bracket();
-        const int D = br >= 0 ? min(G.split_d, G.depth) : 0;
-        int cs, ce;
-        split_chunk(plo, phi, G.split_c, c, &cs, &ce);
-        for (int k = 0; k < (1 << D); ++k) {
-            const int c0 = max(k == 0 ? plo : split_bound(k, D), cs);
-            const int c1 = min(k + 1 == (1 << D) ? phi : split_bound(k + 1, D), ce);
-            const double v = c1 > c0 ? team_sum(range_sum(c0, c1)) : 0.0;   // uniform branch
-            if (tid == 0) out[3 + k] = v;
-        }
-        return;
-    } else
     if constexpr (SWEEP) {
         // Passes share one code instance (register pressure): pass 0 covers (lower, sg1] with
         // the fixed levels and brackets 0, 1, 3's subtrees; later passes one cell of the bracket.
@@ -890,39 +825,15 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
             ++it;
         }
     } else {
-        if (pre_t) {                                       // SPLIT: fixed slabs + the first D levels from
-            split_bracket();                               // the pre-passes' chunk sums
-            stamp(2);
-            stamp(3);
-            nodes += max(G.fix[3] - G.fix[0], 0) + (phi - plo);
-            const int D = br >= 0 ? min(G.split_d, G.depth) : 0;
-            double* cell = (double*)tail;                  // the bracket's cell sums (the tail region is free)
-            if (tid < (1 << D)) cell[tid] = pre_sum(3 + tid);
-            __syncthreads();
-            for (int l = 0, ca = 0, cb = 1 << D; l < D && it < P.K && phi - plo > TCAP; ++l, ++it) {
-                const double mid = (lo + hi) / 2;
-                if (tid == 0) sn[it] = mid;
-                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-                const int cm = (ca + cb) >> 1;
-                double val = 0.0;                          // slab (lo, mid] or (mid, hi]: its cells in order
-                for (int k = ustack ? ca : cm; k < (ustack ? cm : cb); ++k) val += cell[k];
-                const int pm = tr[h];
-                if (level(mid, val)) { lo = mid; plo = pm; ca = cm; }
-                else                 { hi = mid; phi = pm; cb = cm; }
-                h = 2 * h + (ustack ? 1 : 0);
-            }
-            __syncthreads();                               // the cells are read before the tail reuses LDS
-        } else {
-            const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));   // (lower, fg]
-            stamp(2);
-            nodes += max(G.fix[2] - G.fix[0], 0);
-            const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-            const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
-            const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
-            stamp(3);
-            nodes += max(fixpos(nu) - fixpos(nl), 0);
-            bracket(r0, nl, nu, nr);
-        }
+        const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));   // (lower, fg]
+        stamp(2);
+        nodes += max(G.fix[2] - G.fix[0], 0);
+        const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+        stamp(3);
+        nodes += max(fixpos(nu) - fixpos(nl), 0);
+        bracket(r0, nl, nu, nr);
         int pmt = h < tsz ? tr[h] : 0;                     // ub(mid) of heap node h, loaded a level ahead
         for (; it < P.K && phi - plo > TCAP; ++it) {
             const double mid = (lo + hi) / 2;

@@ -28,15 +28,6 @@ struct SortedLaunch {
 
 template <int NT, int COP, bool MSM, int DIM, int PM, bool FUSED, int LAY>
 void sorted_launch_l(const SortedLaunch& L) {
-    if constexpr (NT == kSortNT && LAY != kLay2W) {
-        if (L.mode >= 2) {                             // SPLIT pre-pass: one workgroup per (date, chunk)
-            hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, NT, PM, FUSED, LAY, false, true>),
-                               dim3((unsigned)(L.T * L.G.split_c)), dim3(NT), sorted_lds_bytes(L.S.n, NT, DIM, false, LAY),
-                               L.stream, L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr,
-                               nullptr);
-            return;
-        }
-    }
     if constexpr (DIM == 2 && NT == kSortNT) {
         if (L.sweep && L.mode == 0) {                  // SWEEP: one pass per cell (2-D solves)
             hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, NT, PM, FUSED, LAY, true>), dim3((unsigned)L.T),

@@ -1,6 +1,4 @@
-"""SORTED at 256, 512 and 1024 threads per date (cvq_sorted.hip sorted_threads), and
-SPLIT (cvq_plan.hip split_chunks: two pre-passes sum the fixed slabs and the bracket's
-first levels in C workgroups per date, the solve adds their chunk sums).
+"""SORTED at 256, 512 and 1024 threads per date (cvq_sorted.hip sorted_threads).
 
 A strong-scaling block of a few hundred dates per GPU takes the wider workgroups (the
 launch is latency bound there); a full batch takes 256.  The width changes only how a
@@ -17,9 +15,6 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 WIDTHS = ["256", "512", "1024"]
-# (C chunks per date, D bracket levels from the pre-pass): 1 chunk (same sums, another order),
-# several chunks, D = 0 (fixed slabs only) up to the maximum
-SPLITS = [("1", "4"), ("3", "0"), ("3", "2"), ("4", "5"), ("7", "3")]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -86,60 +81,3 @@ def test_width_full_geometry_identical(cfg, T, monkeypatch):
         assert it == it0, (w, it, it0)
         assert np.array_equal(v, v0), (cfg, w, float(np.max(np.abs(v - v0))))
 
-
-@pytest.mark.parametrize("split", SPLITS)
-@pytest.mark.parametrize("case", ["cfg1", "cfg3_n128", "cfg5_n64", "cfg2_n64", "cfg4_k4_n16", "cfg4_k6_n16",
-                                  "garch_student_n64", "ukf_plackett_n64", "garch3d_student_n16", "q1_lowvol"])
-def test_split_matches_golden(case, split, monkeypatch):
-    from copula_var.engine import QuadraturePlan
-    monkeypatch.setenv("CVQ_SPLIT", "1")
-    monkeypatch.setenv("CVQ_SPLIT_C", split[0])
-    monkeypatch.setenv("CVQ_SPLIT_D", split[1])
-    z = load_golden(case)
-    msm = str(z["model"]) == "msm"
-    vs = z.get("unique_vol_states")
-    per = (z["forecasts_by_states"], z["forecasts"]) if msm else [z["sigma_forecasts"]]
-    p = QuadraturePlan(str(z["model"]), str(z["copula"]), int(z["dim"]), z["x_values"], z["step"], z["densities"],
-                       z["combos"], z["weights"], z["copula_params"], vol_states=vs, strategy="sorted")
-    try:
-        p.set_dates(per)
-        var, it = p.calc_var(float(z["ptf_mean"]))
-    finally:
-        p.close()
-    assert np.array_equal(var, z["var"]), (case, split)
-
-
-@pytest.mark.parametrize("cfg,T", [(3, 625), (5, 625), (4, 250), (2, 125)])
-def test_split_full_geometry_identical(cfg, T, monkeypatch):
-    """SPLIT against the one-kernel solve at full BASELINE geometry, several (C, D), plus the
-    sharded entry point (solve_local + finalize) with the split on."""
-    import torch
-    from copula_var.engine import QuadraturePlan, solve_args
-    c, ipt, uvs, ggp, ptf = _workload(cfg, T)
-    dens, x, step, combos = ggp
-    p = QuadraturePlan(c.model, c.copula, c.dim, x, step, dens, combos, c.weights, c.copula_params(),
-                       vol_states=uvs, strategy="sorted")
-    out = {}
-    try:
-        p.set_dates(ipt)
-        monkeypatch.setenv("CVQ_SPLIT", "0")
-        ref, it0 = p.calc_var(ptf)
-        monkeypatch.setenv("CVQ_SPLIT", "1")
-        for C, D in (("2", "4"), ("5", "5"), ("3", "0")):
-            monkeypatch.setenv("CVQ_SPLIT_C", C)
-            monkeypatch.setenv("CVQ_SPLIT_D", D)
-            out[(C, D)] = p.calc_var(ptf)
-        args = solve_args(ptf)
-        ln, hoff = QuadraturePlan.packed_block_len(args, T)
-        blk = torch.zeros(ln, dtype=torch.float64, device="cuda")
-        var = torch.empty(T, dtype=torch.float64, device="cuda")
-        p.solve_local(args, blk[hoff:].data_ptr(), blk.data_ptr())
-        p.solve_finalize_packed(args, blk.data_ptr(), 1, T, T, var.data_ptr())
-        p.solve_status()
-        out["sharded"] = (var.cpu().numpy(), it0)
-    finally:
-        p.close()
-    assert not np.isnan(ref).any()
-    for k, (v, it) in out.items():
-        assert it == it0, (k, it, it0)
-        assert np.array_equal(v, ref), (cfg, k, float(np.max(np.abs(v - ref))))
