@@ -134,7 +134,7 @@ def main():
             raise SystemExit(f"--nu applies to Student-copula configs; config {a.config} is {cfg.copula}")
         cfg = cfg.with_(nu=float(a.nu))
     if a.strategy == "auto":
-        a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points)
+        a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points, cfg.copula, cfg.copula_params())
     strong = a.global_dates is not None
     T_total = a.global_dates if strong else (a.dates_per_gpu or cfg.T) * world
     sharded = world > 1 or strong                 # local solve -> [all-gather] -> finalize

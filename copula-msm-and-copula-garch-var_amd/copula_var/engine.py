@@ -35,7 +35,17 @@ PREFIX_MAX_N_3D = 64                  # PREFIX solves at most 4096 rows (cvq_pla
 MATERIALISED = ("prefix", "sorted", "sweep")   # strategies that hold only nodes with level <= v_cap
 
 
-def auto_strategy(model: str, dim: int, n: Optional[int] = None) -> str:
+def general_power(copula: Optional[str], copula_params=None) -> bool:
+    """A Student copula whose node power -(nu + 2)/2 is not a half-integer (an IFM-fitted nu):
+    every node takes the general power exp(ex log b) (cvq_special.h pow_node)."""
+    if copula != "student" or copula_params is None:
+        return False
+    nu = float(np.atleast_1d(np.asarray(copula_params, dtype=np.float64))[0])
+    return (nu + 2.0) != np.floor(nu + 2.0)
+
+
+def auto_strategy(model: str, dim: int, n: Optional[int] = None, copula: Optional[str] = None,
+                  copula_params=None) -> str:
     """The measured-fastest strategy per workload (cfg 1-5 on one MI355X)
     among those that run it: COMPACT for 2-asset MSM (cfg 2: 20.3M vs SORTED 16.4M
     VaR-dates/s), SORTED for 2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for
@@ -48,7 +58,9 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None) -> str:
     if dim == 2:
         if n is not None and n > MAX_N:
             raise ValueError(f"num_points <= {MAX_N} (every strategy: cvq_plan_create), got {n}")
-        return "compact" if model == "msm" else "sorted"
+        # a fitted (non-integer) Student nu: SORTED (cfg 2 at nu = 5.364: 9.4M vs COMPACT 7.8M
+        # VaR-dates/s; COMPACT's general-power instance needs 104 VGPRs, 4 waves per SIMD)
+        return "compact" if model == "msm" and not general_power(copula, copula_params) else "sorted"
     if n is None or n <= SORTED_MAX_N[3]:
         return "sorted"
     raise ValueError(f"3-asset grids support num_points <= {SORTED_MAX_N[3]} (SORTED), got {n}")
@@ -93,7 +105,7 @@ class QuadraturePlan:
         self._stream, self._timing, self._counting = None, False, False   # forwarded to the sibling
         self._last: Optional["QuadraturePlan"] = None       # plan of the last device solve (solve_status)
         if strategy == "auto":
-            strategy = auto_strategy(model, self.dim, self._x.size)
+            strategy = auto_strategy(model, self.dim, self._x.size, copula, self._cp)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
                        "compact": N.STRATEGY_COMPACT, "sorted": N.STRATEGY_SORTED,
                        "sweep": N.STRATEGY_SWEEP}[strategy]

@@ -79,6 +79,9 @@ constexpr bool kColgInRow = COP != CVQ_PLACKETT;      // (generic kernel only)
 #define CVQ_COMPACT_ILP 2
 #endif
 constexpr int kIlp = CVQ_COMPACT_ILP;               // independent node chains per row range
+#ifndef CVQ_COMPACT_ILP0
+#define CVQ_COMPACT_ILP0 1                          // node chains of the general (non-integer nu) power
+#endif
 
 // Fixed-level cut table columns: lower, sg0, fg, sg1, vmin, vmax (then padding).
 enum { kCutLower = 0, kCutSg0, kCutFg, kCutSg1, kCutVmin, kCutVmax };
@@ -417,7 +420,7 @@ __device__ __forceinline__ void table_pair(const StaticDev& S, const double* __r
             for (int ax = 0; ax < 2; ++ax) z[ax] = stdtrit_tab_int<NUI>(S.tk, u[ax]);   // student.py:102
 #pragma unroll
             for (int ax = 0; ax < 2; ++ax) {                                            // :164-172
-                const double pw = pow_half_pos(fma(z[ax] * z[ax], S.inv_nu, 1.0), S.uni_m, -S.uni_ex);
+                const double pw = pow_half_pos_c<NUI + 1>(fma(z[ax] * z[ax], S.inv_nu, 1.0));   // uni_m = nu + 1
                 A[ax] = z[ax];
                 B[ax] = isfinite(z[ax]) ? (pdf[ax] * pw) * S.inv_g_uni : pdf[ax] * pos_inf();
             }
@@ -681,7 +684,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             }
         }
         const FastRow fr = load_fast_row<COP, SI>(rowr + RR * rr);
-        constexpr int IL = (COP == CVQ_STUDENT && PM == 0) ? 1 : kIlp;   // general pow: register bound
+        constexpr int IL = (COP == CVQ_STUDENT && PM == 0) ? CVQ_COMPACT_ILP0 : kIlp;   // general pow: register bound
         double acc[IL];
 #pragma unroll
         for (int u = 0; u < IL; ++u) acc[u] = 0.0;

@@ -123,7 +123,7 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
     marginal_u<MSM>(S, a, td, d, i, &u, &pdf);
     if constexpr (COP == CVQ_STUDENT && TAB && NUI > 0 && CVQ_TABLE_INT_NU) {
         const double z = stdtrit_tab_int<NUI>(S.tk, u);                              // student.py:102
-        const double pw = pow_half_pos(fma(z * z, S.inv_nu, 1.0), S.uni_m, -S.uni_ex);   // :164-172
+        const double pw = pow_half_pos_c<NUI + 1>(fma(z * z, S.inv_nu, 1.0));            // :164-172, uni_m = nu + 1
         *A_out = z;
         *B_out = isfinite(z) ? (pdf * pw) * S.inv_g_uni : pdf * pos_inf();
         return;
@@ -134,7 +134,7 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
     } else {
         double z, uni;
         if (COP == CVQ_STUDENT) {
-            z = TAB ? stdtrit_tabulated(S.tk, u) : stdtrit(S.tk, u);   // student.py:102
+            z = TAB ? stdtrit_tab_bf(S.tk, u) : stdtrit(S.tk, u);   // student.py:102
             uni = isfinite(z) ? S.g_uni * pow_half_neg(1.0 + (z * z) / S.nu, S.uni_m, S.uni_ex) : 0.0;   // :164-172
         } else {
             z = ndtri(u);                                        // gaussian.py:44

@@ -306,12 +306,16 @@ __host__ __device__ __forceinline__ double stdtrit_tabulated(const TConst& k, do
 // stdtrit_tabulated without data-dependent branches: the same arithmetic (both
 // table variables evaluated, one selected), so a thread can keep two
 // evaluations' table gathers in flight together.
+__device__ __forceinline__ double log_node(double b);
+__device__ __forceinline__ double exp_node(double x);
 __device__ __forceinline__ double stdtrit_tab_bf(const TConst& k, double p) {
     const bool upper = p > 0.5;
     const double pp = upper ? (1.0 - p) : p;                   // exact
     const bool centre = pp >= k.p_split;
     const double d = 0.5 - pp;
-    const double v = exp(log(pp) * k.inv_nu);
+    // tail variable pp^(1/nu) without library calls (log_node / exp_node, ~1e-14; pp = 0 and NaN
+    // are replaced below)
+    const double v = exp_node(log_node(pp) * k.inv_nu);
     const double q = centre ? quintic(k.q_c, k.n_qc, d * k.inv_qc) : quintic(k.q_v, k.n_qv, v * k.inv_qv);
     double t = centre ? d * q : -1.0 / (v * q);
     t = upper ? -t : t;
@@ -406,7 +410,7 @@ __device__ __forceinline__ double exp_node(double x) {
     return __builtin_amdgcn_ldexp(p, (int)k);
 }
 
-// log(b) for finite b >= 1 (the node power's base): b = 2^k m, m in [sqrt(1/2), sqrt(2)),
+// log(b) for finite b > 0 (the node power base, the quantile tail pp): b = 2^k m, m in [sqrt(1/2), sqrt(2)),
 // log(1 + f) from s = f / (2 + f) and the published fdlibm e_log.c minimax polynomial in s^2
 // (< 1 ulp there; the reciprocal here is v_rcp_f64 + two Newton steps, ~1 ulp more), no
 // branches or library calls.
@@ -418,17 +422,23 @@ __device__ __forceinline__ double log_node(double b) {
     k = lo ? k - 1 : k;
     const double f = m - 1.0;
     const double s = f * fast_rcp(2.0 + f);
-    const double z = s * s, w = z * z;
-    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
-    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
-                                     2.857142874366239149e-01), 6.666666666666735130e-01);
-    const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+    const double z = s * s;
+    // R = Lg1 z + ... + Lg7 z^7 as one Horner chain (fewer live values than fdlibm's even / odd split)
+    double R = fma(z, 1.479819860511658591e-01, 1.531383769920937332e-01);
+    R = fma(z, R, 1.818357216161805012e-01);
+    R = fma(z, R, 2.222219843214978396e-01);
+    R = fma(z, R, 2.857142874366239149e-01);
+    R = fma(z, R, 3.999999999940941908e-01);
+    R = fma(z, R, 6.666666666666735130e-01);
+    R *= z;
+    const double hfsq = 0.5 * f * f, dk = (double)k;
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
 #ifndef CVQ_POW_LIB
 #define CVQ_POW_LIB 0
 #endif
+__device__ __forceinline__ double pow_gen(double b, double ex);
 // b^ex for b >= 1 with ex = -m/2 (m = node_m >= 0): squarings + one reciprocal;
 // m < 0 (non-integer nu: an IFM-fitted copula) selects exp(ex log b) from log_node / exp_node
 // (~1e-14 relative; the OCML pair cost ~210 instructions per node in the solve kernels' node
@@ -444,13 +454,19 @@ __device__ __forceinline__ double pow_node(double b, int m, double ex) {
         return fast_rcp(r);
     }
     if (CVQ_POW_LIB) return exp(ex * log(b));
-    const double y = exp_node(ex * log_node(b));
-    return (b < 1.0e300) ? y : (b == b ? 0.0 : b);          // b^ex, ex <= -1/2: +inf -> 0, NaN stays NaN
+    return pow_gen(b, ex);                                   // ex <= -1/2: +inf -> 0, NaN stays NaN
 }
 
-// b^(-m/2) for b >= 1, general m >= 0 (m < 0: exp(ex log b)); no loop for m <= 16.
+// b^ex for b >= 1 from log_node / exp_node (~1e-14 relative, no library calls); b = +inf gives
+// 0 (ex < 0) or +inf, NaN stays NaN
+__device__ __forceinline__ double pow_gen(double b, double ex) {
+    const double y = exp_node(ex * log_node(b));
+    return (b < 1.0e300) ? y : (b == b ? (ex < 0.0 ? 0.0 : b) : b);
+}
+
+// b^(-m/2) for b >= 1, general m >= 0 (m < 0: b^ex, ex = -(nu+1)/2); no loop for m <= 16.
 __device__ __forceinline__ double pow_half_neg(double b, int m, double ex) {
-    if (m < 0 || m > 16) return exp(ex * log(b));
+    if (m < 0 || m > 16) return pow_gen(b, ex);
     const double b2 = b * b, b4 = b2 * b2, b8 = b4 * b4;
     const int k = m >> 1;
     double r = (k & 1) ? b : 1.0;
@@ -462,10 +478,23 @@ __device__ __forceinline__ double pow_half_neg(double b, int m, double ex) {
     return 1.0 / r;
 }
 
+// b^(M/2) for a compile-time M >= 0 (the integer-nu tables: M = nu + 1)
+template <int M>
+__device__ __forceinline__ double pow_half_pos_c(double b) {
+    double r = 1.0, s = b;
+#pragma unroll
+    for (int k = M >> 1; k; k >>= 1) {
+        if (k & 1) r *= s;
+        s *= s;
+    }
+    if constexpr (M & 1) r *= sqrt(b);
+    return r;
+}
+
 // b^(m/2) for b >= 1, general m >= 0 (m < 0: exp(ex log b)), the reciprocal of pow_half_neg
 // without its division (ex = +(nu+1)/2 here)
 __device__ __forceinline__ double pow_half_pos(double b, int m, double ex) {
-    if (m < 0 || m > 16) return exp(ex * log(b));
+    if (m < 0 || m > 16) return pow_gen(b, ex);
     const double b2 = b * b, b4 = b2 * b2, b8 = b4 * b4;
     const int k = m >> 1;
     double r = (k & 1) ? b : 1.0;

@@ -15,6 +15,12 @@ def test_auto_strategy_rules():
     assert auto_strategy("msm", 3, 128) == "sorted"
     assert auto_strategy("garch", 3, 255) == "sorted"
     assert auto_strategy("msm", 2) == "compact"            # n unknown: the 2-D rule
+    # a fitted Student nu (general node power): SORTED for MSM too; nu = 6 or any integer: COMPACT
+    assert auto_strategy("msm", 2, 256, "student", [5.364, 0.5]) == "sorted"
+    assert auto_strategy("msm", 2, 256, "student", [6.0, 0.5]) == "compact"
+    assert auto_strategy("msm", 2, 256, "student", [5.0, 0.5]) == "compact"   # nu + 2 integer: no log / exp
+    assert auto_strategy("msm", 2, 256, "student", [4.5, 0.5]) == "sorted"
+    assert auto_strategy("msm", 2, 256, "gaussian", [0.5]) == "compact"
     with pytest.raises(ValueError):
         auto_strategy("msm", 3, 256)                        # no 3-D strategy takes n > 255
 
