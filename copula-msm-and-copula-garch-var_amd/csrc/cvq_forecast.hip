@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "cvq_common.h"
@@ -35,6 +36,10 @@ struct MsmParams {
 
 struct MsmParamsN {
     MsmParams a[3];                                // per asset (dim <= 3), passed by value
+};
+
+struct StateMap {
+    uint8_t u[3][128];                             // unique-vol index of state s of asset d
 };
 
 struct StateMapQ {                                 // unique-vol index of each of <= 16 states, per asset
@@ -75,6 +80,61 @@ __device__ __forceinline__ double quad_xor(double v) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
+}
+
+// Lane exchanges for a state vector spread one state per lane over a wavefront: v of lane
+// (l xor M).  M = 1, 2: quad_perm; M = 4, 8: row_shl / row_shr by M selected by lane bit M (DPP,
+// VALU moves with no LDS round trip); M = 16, 32: ds_bpermute (__shfl_xor).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int M>
+__device__ __forceinline__ double lane_xor(double v) {
+    if constexpr (M == 1) return dpp_f64<0xB1>(v);
+    else if constexpr (M == 2) return dpp_f64<0x4E>(v);
+    else if constexpr (M == 4 || M == 8) {
+        const double up = dpp_f64<0x100 | M>(v), dn = dpp_f64<0x110 | M>(v);   // row_shl:M / row_shr:M
+        return (threadIdx.x & M) ? dn : up;
+    } else {
+        // v_permlane16_swap / v_permlane32_swap (gfx950, VALU): with both operands v, lane l of the
+        // swapped src (lanes below the half) or of vdst (lanes above) holds v of lane l xor M
+        const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+        const bool up = (threadIdx.x & M) != 0;
+        unsigned nlo, nhi;
+        if constexpr (M == 16) {
+            const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            nlo = up ? a[0] : a[1];
+            nhi = up ? b[0] : b[1];
+        } else {
+            const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+            const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+            nlo = up ? a[0] : a[1];
+            nhi = up ? b[0] : b[1];
+        }
+        return __hiloint2double((int)nhi, (int)nlo);
+    }
+}
+// sum over the 64 lanes, in every lane: DPP inclusive scan (row_shr 1, 2, 4, 8, row_bcast 15, 31),
+// then lane 63's total broadcast
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_f64z(double v) {         // bound_ctrl: out-of-row lanes read 0
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RM, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RM, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_total(double v) {
+    v += dpp_f64z<0x111, 0xF>(v);
+    v += dpp_f64z<0x112, 0xF>(v);
+    v += dpp_f64z<0x114, 0xF>(v);
+    v += dpp_f64z<0x118, 0xF>(v);
+    v += dpp_f64z<0x142, 0xA>(v);
+    v += dpp_f64z<0x143, 0xC>(v);
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                            __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
 template <int K>
@@ -404,6 +464,14 @@ __global__ __launch_bounds__(64) void k_msm_windows(MsmParamsN PN, const double*
 constexpr int kScanB = CVQ_SCAN_B;   // steps per block (the block scan's serial chain)
 constexpr int kScanC = CVQ_SCAN_C;   // blocks per superblock (the superblock scan's serial chain)
 
+// k = 5, 6 (32 / 64 states, BASELINE config 4's k = 6): the same factorisation with the block
+// prefixes left out -- a window runs its last partial block (<= B steps) as filter steps on the
+// vector instead of reading a stored S x S prefix per window end (T S^2 doubles: 196 MB at cfg 4)
+// -- and the matrices stored column-major so a window's lanes (one state each) read a factor
+// column in one coalesced load (k_msm_supscan_w, k_msm_scanwin_w).
+template <int K>
+constexpr bool kWideScan = K >= 5;
+
 // v <- A v for a quad-resident state vector (the transition of calc_prob.py:91-101 as k
 // Kronecker butterflies; A is symmetric, so this is also v^T A for a row vector)
 template <int K>
@@ -493,15 +561,21 @@ __global__ __launch_bounds__(4 << K) void k_msm_blkscan(MsmParamsN PN, const dou
             apply_A<K>(v, P);
 #pragma unroll
             for (int j = 0; j < SL; ++j) v[j] = v[j] * (cl[o * S + lane_q * SL + j] * sc);
-            if (i >= n_in - 1) {
+            if (!kWideScan<K> && i >= n_in - 1) {
                 double* dst = pre + ((i - (n_in - 1)) * S + lane_q * SL) * S + q;
 #pragma unroll
                 for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
             }
             if (o == kScanB - 1) {                               // a full block's product G_b
-                double* dst = Gf + blockIdx.y * gstride + (blockIdx.x * (long long)S + lane_q * SL) * S + q;
+                if constexpr (kWideScan<K>) {                    // column-major: column q is contiguous
+                    double* dst = Gf + blockIdx.y * gstride + (blockIdx.x * (long long)S + q) * S + lane_q * SL;
 #pragma unroll
-                for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
+                    for (int j = 0; j < SL; ++j) dst[j] = v[j];
+                } else {
+                    double* dst = Gf + blockIdx.y * gstride + (blockIdx.x * (long long)S + lane_q * SL) * S + q;
+#pragma unroll
+                    for (int j = 0; j < SL; ++j) dst[j * S] = v[j];
+                }
             }
         }
     } else {                                                     // Suf: rows, backward
@@ -735,15 +809,293 @@ __global__ __launch_bounds__(256) void k_msm_scanwin(const double* __restrict__ 
     fbs[(t * dim + d) * M.q + g] = f;
 }
 
+// Superblock prefix / suffix products for 32 or 64 states: the running product X (S x S, a
+// (S/16) x (S/16) block per thread of 256) times the next block product G_b staged in LDS
+// (rows padded by one double: a column read by the 16 block-rows of a wave hits 16 banks),
+// then scaled by its maximum over the workgroup.  z = 0: PG_s(beta) = G_{sC+beta} ... G_{sC}
+// (X <- G X); z = 1: SG_s(beta) = G_{last} ... G_{sC+beta} (X <- X G).  Column-major I/O.
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_supscan_w(const double* __restrict__ Gf, long long gstride,
+                                                       long long nfull, double* __restrict__ PG,
+                                                       double* __restrict__ SG, long long sstride) {
+    constexpr int S = 1 << K, SP = S + 2, RB = S / 16;      // RB x RB block of X per thread
+    static_assert(RB % 2 == 0, "16-B LDS reads of pairs");
+    __shared__ __attribute__((aligned(16))) double Gs[S * SP], Xs[S * SP];
+    __shared__ double wmax[4];
+    const int tid = threadIdx.x, br = tid / 16, bc = tid % 16;
+    const long long s0 = (long long)blockIdx.x * kScanC, s1 = min(s0 + kScanC, nfull);
+    Gf += blockIdx.y * gstride;
+    double* out = (blockIdx.z == 0 ? PG : SG) + blockIdx.y * sstride;
+    double x[RB][RB];
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) x[a][b] = (br * RB + a == bc * RB + b) ? 1.0 : 0.0;
+    const bool fwd = blockIdx.z == 0;
+    constexpr int GE = S * S / 256;
+    double gn[GE];                                               // the next block product, loaded a step ahead
+    const long long nst = s1 - s0;
+    auto gload = [&](long long it) {
+        const double* G = Gf + (fwd ? s0 + it : s1 - 1 - it) * S * S;   // column-major: G[c * S + r] = G_b(r, c)
+#pragma unroll
+        for (int m = 0; m < GE; ++m) gn[m] = G[tid + 256 * m];
+    };
+    if (nst > 0) gload(0);
+    for (long long it = 0; it < nst; ++it) {
+        const long long bidx = fwd ? s0 + it : s1 - 1 - it;
+#pragma unroll
+        for (int m = 0; m < GE; ++m) {
+            const int e = tid + 256 * m, c = e / S, r = e % S;
+            Gs[r * SP + c] = gn[m];
+        }
+        if (it + 1 < nst) gload(it + 1);
+#pragma unroll
+        for (int a = 0; a < RB; ++a)
+#pragma unroll
+            for (int b = 0; b < RB; ++b) Xs[(br * RB + a) * SP + bc * RB + b] = x[a][b];
+        __syncthreads();
+        double y[RB][RB];
+#pragma unroll
+        for (int a = 0; a < RB; ++a)
+#pragma unroll
+            for (int b = 0; b < RB; ++b) y[a][b] = 0.0;
+        // forward Y = G X: u = G(i, c), w = X(c, j); backward Y = X G: u = X(i, c), w = G(c, j);
+        // two c per round, every operand a 16-B LDS read (rows padded to S + 2: aligned pairs,
+        // the 4 block-rows of a wave on distinct banks)
+        const double* U = fwd ? Gs : Xs;
+        const double* W = fwd ? Xs : Gs;
+#pragma unroll 2
+        for (int c = 0; c < S; c += 2) {
+            double2 u[RB], w0[RB / 2], w1[RB / 2];
+#pragma unroll
+            for (int a = 0; a < RB; ++a) u[a] = *(const double2*)&U[(br * RB + a) * SP + c];
+#pragma unroll
+            for (int b = 0; b < RB / 2; ++b) {
+                w0[b] = *(const double2*)&W[c * SP + bc * RB + 2 * b];
+                w1[b] = *(const double2*)&W[(c + 1) * SP + bc * RB + 2 * b];
+            }
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+                for (int b = 0; b < RB / 2; ++b) {
+                    y[a][2 * b] = fma(u[a].x, w0[b].x, y[a][2 * b]);
+                    y[a][2 * b + 1] = fma(u[a].x, w0[b].y, y[a][2 * b + 1]);
+                    y[a][2 * b] = fma(u[a].y, w1[b].x, y[a][2 * b]);
+                    y[a][2 * b + 1] = fma(u[a].y, w1[b].y, y[a][2 * b + 1]);
+                }
+        }
+        double m = 0.0;
+#pragma unroll
+        for (int a = 0; a < RB; ++a)
+#pragma unroll
+            for (int b = 0; b < RB; ++b) m = fmax(m, y[a][b]);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        if ((tid & 63) == 0) wmax[tid >> 6] = m;
+        __syncthreads();                                         // also: every read of Gs / Xs is done
+        const double sc = 1.0 / fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3]));
+        double* dst = out + bidx * S * S;
+#pragma unroll
+        for (int a = 0; a < RB; ++a)
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+                x[a][b] = y[a][b] * sc;
+                dst[(bc * RB + b) * S + br * RB + a] = x[a][b];
+            }
+        __syncthreads();                                         // wmax is rewritten by the next step
+    }
+}
+
+// Windows for 32 or 64 states, 16 consecutive windows per workgroup (t0 = 16 g: one start
+// block b0, so one lo_b, and ends in at most two blocks).  Lane s of each wave = state s, a wave
+// holds 4 windows.  Per window: its first partial block [t, (b0 + 1) B) as filter steps from the
+// uniform prior (calc_prob.py:12-13, 51-69: butterflies by lane xor, c_i from the returns), the
+// full blocks lo_b .. H shared by the group (H = the group's smallest hi_b; each factor staged
+// once in LDS, column-major, and applied to all 16 vectors), one more block product G_{H+1} for
+// the windows whose hi_b = H + 1, then its last partial block [b1 B, e] as filter steps, and the
+// collapse onto the asset's unique vols in state order (Q14) into fbs.  Every vector normalised
+// after each factor / step (positive factors cancel).
+constexpr int kWinGroup = 16;                                    // windows per workgroup = kScanB
+template <int K>
+__global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const double* __restrict__ r, long long N,
+                                                       const double* __restrict__ Gf, long long gstride,
+                                                       const double* __restrict__ PG, const double* __restrict__ SG,
+                                                       long long sstride, long long nfull, long long n_in,
+                                                       long long T, StateMap M, int q, int dim,
+                                                       double* __restrict__ fbs) {
+    constexpr int S = 1 << K, WPW = 4;                           // states, windows per wave
+    static_assert(S <= 64 && kWinGroup == 4 * WPW && kWinGroup == kScanB, "16 windows, one start block");
+    __shared__ __attribute__((aligned(16))) double Fs[S * S];    // the factor, column-major
+    __shared__ __attribute__((aligned(16))) double xs[4][S][WPW];   // per wave: x_m[c] of its 4 windows
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, s = lane < S ? lane : 0;
+    const bool act = lane < S;
+    const int d = blockIdx.y;
+    const MsmParams& P = PN.a[d];
+    r += d * N;
+    Gf += d * gstride;
+    PG += d * sstride;
+    SG += d * sstride;
+    const long long t0 = (long long)blockIdx.x * kWinGroup;
+    long long tw[WPW];
+    bool live[WPW];
+#pragma unroll
+    for (int m = 0; m < WPW; ++m) {
+        tw[m] = t0 + wv * WPW + m;
+        live[m] = tw[m] < T;
+    }
+    double x[WPW];
+    auto wsum = [&](double v) { return wave_total(act ? v : 0.0); };   // over the wave's S state lanes
+    // filter steps i in [i0, i1) (i1 - i0 <= 64) for window m when i lies in its range [a_m, b_m);
+    // the returns r[i0 ..] are loaded once, one per lane, and broadcast by readlane
+    auto steps = [&](long long i0, long long i1, const long long (&a)[WPW], const long long (&b)[WPW]) {
+        const double rl = (i0 + lane < i1) ? r[i0 + lane] : 0.0;
+#pragma unroll 1
+        for (long long i = i0; i < i1; ++i) {
+            const int li = (int)(i - i0);
+            const double ri = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(rl), li),
+                                               __builtin_amdgcn_readlane(__double2loint(rl), li));
+            const double ci = act ? cond_prob(ri, P.vs[s]) : 0.0;
+#pragma unroll
+            for (int m = 0; m < WPW; ++m) {
+                const bool on = i >= a[m] && i < b[m];           // wave-uniform
+                double v = x[m];
+                auto bfly = [&](auto cc) {                       // component c <-> state bit K-1-c
+                    constexpr int c = decltype(cc)::value;
+                    const double o = lane_xor<(1 << (K - 1 - c))>(v);
+                    v = P.p[c] * v + P.qv[c] * o;
+                };
+                bfly(std::integral_constant<int, 0>{});
+                bfly(std::integral_constant<int, 1>{});
+                bfly(std::integral_constant<int, 2>{});
+                bfly(std::integral_constant<int, 3>{});
+                bfly(std::integral_constant<int, 4>{});
+                if constexpr (K == 6) bfly(std::integral_constant<int, 5>{});
+                v *= ci;
+                const double tot = wsum(v);
+                if (on) x[m] = v * (1.0 / tot);
+            }
+        }
+    };
+    // 1. first partial block: [t, (b0 + 1) B) from the uniform prior
+    const long long b0 = t0 / kScanB, bend = (b0 + 1) * kScanB;
+    {
+        long long a[WPW], b[WPW];
+#pragma unroll
+        for (int m = 0; m < WPW; ++m) {
+            x[m] = 1.0 / S;
+            a[m] = tw[m];
+            b[m] = bend;
+        }
+        steps(a[0], bend, a, b);                                 // this wave's first window starts at a[0]
+    }
+    // 2. full blocks lo_b .. H (shared), then G_{H+1} for the windows with hi_b = H + 1
+    const long long lo_b = b0 + 1, H = (t0 + n_in - 1) / kScanB - 1;
+    long long hib[WPW];
+#pragma unroll
+    for (int m = 0; m < WPW; ++m) hib[m] = (tw[m] + n_in - 1) / kScanB - 1;
+    const long long sa = lo_b / kScanC, sb = H / kScanC;
+    int kind;                                                    // as k_msm_scanwin, for (lo_b, H)
+    long long cnt;
+    if (lo_b > H) { kind = 0; cnt = 0; }
+    else if (sa == sb) {
+        const long long send = min(sa * kScanC + kScanC, nfull) - 1;
+        kind = lo_b == sa * kScanC ? 1 : (H == send ? 2 : 3);
+        cnt = kind == 3 ? H - lo_b + 1 : 1;
+    } else { kind = 4; cnt = sb - sa + 1; }
+    auto mat = [&](long long k) -> const double* {
+        if (k == cnt) return Gf + (H + 1) * S * S;               // the extra block (some windows)
+        switch (kind) {
+            case 1: return PG + (sa * kScanC + (H - sa * kScanC)) * S * S;
+            case 2: return SG + (sa * kScanC + (lo_b - sa * kScanC)) * S * S;
+            case 3: return Gf + (lo_b + k) * S * S;
+            default:
+                if (k == 0) return SG + (sa * kScanC + (lo_b - sa * kScanC)) * S * S;
+                if (k == cnt - 1) return PG + (sb * kScanC + (H - sb * kScanC)) * S * S;
+                return SG + ((sa + k) * kScanC) * S * S;          // full superblock sa + k
+        }
+    };
+    bool extra = false;                                          // any window of the group needs G_{H+1}
+#pragma unroll
+    for (int m = 0; m < WPW; ++m) extra |= live[m] && hib[m] == H + 1;
+    extra = __syncthreads_or(extra);
+    const long long nf = cnt + (extra ? 1 : 0);
+    constexpr int FE = S * S / 256;                              // factor entries per thread
+    double fn[FE];                                               // the next factor, loaded a factor ahead
+    if (nf > 0) {
+        const double* F = mat(0);
+#pragma unroll
+        for (int e = 0; e < FE; ++e) fn[e] = F[tid + 256 * e];
+    }
+    for (long long k = 0; k < nf; ++k) {
+#pragma unroll
+        for (int e = 0; e < FE; ++e) Fs[tid + 256 * e] = fn[e];
+        if (k + 1 < nf) {
+            const double* F = mat(k + 1);
+#pragma unroll
+            for (int e = 0; e < FE; ++e) fn[e] = F[tid + 256 * e];
+        }
+        if (act) {
+#pragma unroll
+            for (int m = 0; m < WPW; ++m) xs[wv][s][m] = x[m];
+        }
+        __syncthreads();
+        double y[WPW] = {};
+#pragma unroll 4
+        for (int c = 0; c < S; ++c) {
+            const double f = Fs[c * S + s];
+            const double2 x01 = *(const double2*)&xs[wv][c][0];  // broadcast reads
+            const double2 x23 = *(const double2*)&xs[wv][c][2];
+            y[0] = fma(f, x01.x, y[0]);
+            y[1] = fma(f, x01.y, y[1]);
+            y[2] = fma(f, x23.x, y[2]);
+            y[3] = fma(f, x23.y, y[3]);
+        }
+#pragma unroll
+        for (int m = 0; m < WPW; ++m) {
+            const double tot = wsum(y[m]);
+            if (k < cnt || hib[m] == H + 1) x[m] = y[m] * (1.0 / tot);
+        }
+        __syncthreads();                                         // Fs / xs rewritten by the next factor
+    }
+    // 3. last partial block [b1 B, e] of each window
+    {
+        long long a[WPW], b[WPW], lo = 1LL << 62, hi = 0;
+#pragma unroll
+        for (int m = 0; m < WPW; ++m) {
+            const long long e = tw[m] + n_in - 1;
+            a[m] = (e / kScanB) * kScanB;
+            b[m] = live[m] ? e + 1 : a[m];
+            lo = min(lo, a[m]);
+            hi = max(hi, b[m]);
+        }
+        if (hi > lo) steps(lo, hi, a, b);
+    }
+    // 4. collapse onto unique vols, states in order (Q14): lane u < q of the wave sums its
+    // windows' states mapped to u (the vectors through LDS; the last barrier freed xs)
+    if (act) {
+#pragma unroll
+        for (int m = 0; m < WPW; ++m) xs[wv][s][m] = x[m];
+    }
+    __syncthreads();
+    if (lane < q) {
+        double f[WPW] = {};
+#pragma unroll 1
+        for (int c = 0; c < S; ++c) {
+            if (M.u[d][c] != lane) continue;
+#pragma unroll
+            for (int m = 0; m < WPW; ++m) f[m] += xs[wv][c][m];
+        }
+#pragma unroll
+        for (int m = 0; m < WPW; ++m)
+            if (live[m]) fbs[(tw[m] * dim + d) * q + lane] = f[m];
+    }
+}
+
 // sum_forecast_by_state (msm_estimation.py:205-248, Q14) + compute_forecast_combinations
 // (:392-418, Q7) on the device.  filt [dim][T][S] -> fbs [T][dim][q]
 // (states collapsed onto their unique 1e-6-rounded vol, summed in state order) and
 // pi [T][q^dim] in the reference's xy-meshgrid product order (2-D: f0[a] f1[b];
 // 3-D: (f0[L1] f1[L2]) f2[L0]).
-struct StateMap {
-    uint8_t u[3][128];                             // unique-vol index of state s of asset d
-};
-
 // One thread per output: k_msm_fbs, thread per (date, asset), the
 // states of its filtered vector summed onto their unique vols in state order; k_msm_pi,
 // thread per (date, combination), the product in the reference's meshgrid order.
@@ -1239,10 +1591,12 @@ int launch_blocked_k(int k, const MsmParamsN& P, int dim, const double* cond, lo
 }
 
 // Transfer-matrix scan filter (k_msm_blkscan -> k_msm_supscan -> k_msm_scanwin): 2 <= k <= 4
-// (one wavefront per superblock scan) and windows longer than two blocks.
+// (one wavefront per superblock scan); k = 5, 6 the wide variant (no stored prefixes, 256-thread
+// superblock scans, one wavefront per window); windows longer than two blocks.
 bool msm_scan_ok(int k, long long n_in) {
     static const bool on = !getenv("CVQ_MSM_SCAN") || atoi(getenv("CVQ_MSM_SCAN")) != 0;   // A/B switch
-    return on && k >= 2 && k <= 4 && n_in > 2 * kScanB;
+    static const bool wide = !getenv("CVQ_MSM_SCAN_WIDE") || atoi(getenv("CVQ_MSM_SCAN_WIDE")) != 0;
+    return on && k >= 2 && (k <= 4 || (wide && k <= 6)) && n_in > 2 * kScanB;
 }
 
 struct ScanLayout {                 // doubles of each scan buffer, per asset
@@ -1253,8 +1607,8 @@ ScanLayout scan_layout(int k, long long n_in, long long T) {
     ScanLayout L;
     L.nfull = N / kScanB;
     L.nsup = (L.nfull + kScanC - 1) / kScanC;
-    L.pre = T * S * S;
-    L.suf = T * S;
+    L.pre = k >= 5 ? 0 : T * S * S;                 // the wide scan stores no block prefixes
+    L.suf = k >= 5 ? 0 : T * S;                     // (nor window-start suffixes)
     L.gf = L.nfull * S * S;
     L.sup = L.nsup * kScanC * S * S;
     return L;
@@ -1286,6 +1640,26 @@ void launch_scan(const MsmParamsN& P, const StateMapQ& MQ, int dim, const double
                            L.gf, L.nfull, PG, SG, L.sup);
     hipLaunchKernelGGL(k_msm_scanwin<K>, dim3((unsigned)((T + 15) / 16), (unsigned)dim), dim3(256), 0, stream, Pre,
                        L.pre, Suf1, L.suf, Gf, L.gf, PG, SG, L.sup, L.nfull, n_in, T, MQ, dim, fbs);
+}
+
+template <int K>
+void launch_scan_w(const MsmParamsN& P, const StateMap& M, int q, int dim, const double* r, long long N,
+                   long long n_in, long long T, double* buf, double* fbs, int* err, hipStream_t stream) {
+    constexpr int S = 1 << K;
+    const ScanLayout L = scan_layout(K, n_in, T);
+    double* Suf1 = buf;                                         // L.pre = 0: no prefixes
+    double* Gf = Suf1 + dim * L.suf;
+    double* PG = Gf + dim * L.gf;
+    double* SG = PG + dim * L.sup;
+    const long long nblk = (N + kScanB - 1) / kScanB;
+    // block products only (z = 0): a window runs its first partial block as filter steps
+    hipLaunchKernelGGL(k_msm_blkscan<K>, dim3((unsigned)nblk, (unsigned)dim, 1), dim3(4 * S), 0, stream, P, r, N,
+                       n_in, T, nullptr, 0LL, Suf1, L.suf, Gf, L.gf, err);
+    if (L.nsup > 0)
+        hipLaunchKernelGGL(k_msm_supscan_w<K>, dim3((unsigned)L.nsup, (unsigned)dim, 2), dim3(256), 0, stream, Gf,
+                           L.gf, L.nfull, PG, SG, L.sup);
+    hipLaunchKernelGGL(k_msm_scanwin_w<K>, dim3((unsigned)((T + kWinGroup - 1) / kWinGroup), (unsigned)dim),
+                       dim3(256), 0, stream, P, r, N, Gf, L.gf, PG, SG, L.sup, L.nfull, n_in, T, M, q, dim, fbs);
 }
 
 int launch_scan_k(int k, const MsmParamsN& P, const StateMapQ& MQ, int dim, const double* r, long long N,
@@ -1373,11 +1747,17 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
     // step-by-step and blocked filters OR into the error word, reset here
     if (!scan) CVQ_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int), st));
     if (scan) {                        // densities computed per block inside; the collapse fused into the windows
-        StateMapQ MQ{};
+        StateMapQ MQ{};                                  // k <= 4: <= 16 states
         MQ.q = q;
-        for (int d = 0; d < dim; ++d)
+        for (int d = 0; d < dim && S <= 16; ++d)
             for (int s2 = 0; s2 < S; ++s2) MQ.u[d][s2] = M.u[d][s2];
-        rc = launch_scan_k(k, P, MQ, dim, returns_c, N, n_in, T, G, fbs_out, err + 4, st);
+        if (k >= 5) {
+            if (k == 5) launch_scan_w<5>(P, M, q, dim, returns_c, N, n_in, T, G, fbs_out, err + 4, st);
+            else launch_scan_w<6>(P, M, q, dim, returns_c, N, n_in, T, G, fbs_out, err + 4, st);
+            CVQ_HIP_CHECK(hipGetLastError());
+        } else {
+            rc = launch_scan_k(k, P, MQ, dim, returns_c, N, n_in, T, G, fbs_out, err + 4, st);
+        }
         if (rc) return rc;
     } else {
         hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), (unsigned)dim), dim3(256), 0, st, P, S,

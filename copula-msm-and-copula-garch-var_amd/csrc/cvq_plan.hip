@@ -1424,6 +1424,17 @@ int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
     return CVQ_OK;
 }
 
+int32_t cvq_plan_debug_nodes(cvq_plan* p, uint32_t* host, int64_t count, int32_t* fix) {
+    CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(p->d_pidx != nullptr && p->tree_valid, CVQ_ERR_STATE,
+                "no solve-order node list (a SORTED plan builds it at its first solve)");
+    CVQ_REQUIRE(count <= (int64_t)p->S.G, CVQ_ERR_INVALID, "count exceeds the plan's reachable nodes");
+    CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
+    CVQ_HIP_CHECK(hipMemcpy(host, p->d_pidx, count * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (fix) for (int e = 0; e < 6; ++e) fix[e] = p->fixpos[e];
+    return CVQ_OK;
+}
+
 int32_t cvq_plan_count_nodes(cvq_plan* p, int32_t enable) {
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
     CVQ_REQUIRE(!enable || p->strategy == CVQ_STRATEGY_COMPACT || p->strategy == CVQ_STRATEGY_SORTED ||

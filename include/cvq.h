@@ -118,6 +118,10 @@ int32_t cvq_plan_kernel_time(cvq_plan* plan, int32_t kind, double* total_ms, int
  * solve, recorded only when the process runs with CVQ_STAMPS=1 (never in a timed
  * run).  host receives count uint64 values, 32 per date. */
 int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
+/* Diagnostic: the SORTED plan's node words in solve order (first `count` of its reachable
+   nodes; the LDS byte offsets of their records, cvq_sorted_kernels.h sorted_pack) and, when
+   fix != NULL, the sorted positions of the six fixed levels of the last solve's arguments. */
+int32_t cvq_plan_debug_nodes(cvq_plan* plan, uint32_t* host, int64_t count, int32_t* fix);
 /* Measurement aid (bench.py's FP64 roofline basis): with cvq_plan_count_nodes(plan, 1)
  * the following COMPACT / SORTED / SWEEP solves record how many quadrature nodes each
  * date evaluated (the phase-stamp buffer: slower, never in a timed run);

@@ -186,3 +186,21 @@ def test_scan_filter_window_shapes(n_in, T):
     np.testing.assert_array_equal(uvs_d, uvs)
     np.testing.assert_allclose(mt.fbs.cpu().numpy(), fbs, rtol=1e-12, atol=1e-300)
     np.testing.assert_allclose(mt.pi.cpu().numpy(), pi, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize("cfg_no,k,n_in,T", [(4, 6, 1135, 200), (4, 6, 70, 50), (4, 6, 600, 300), (4, 6, 1135, 1),
+                                             (2, 5, 1135, 300), (2, 5, 100, 17), (2, 6, 300, 64)])
+def test_wide_scan_filter_k5_k6(cfg_no, k, n_in, T):
+    """k = 5, 6 (BASELINE config 4's 64 states): the wide transfer-matrix scan (block products,
+    superblock scans over 64 x 64 matrices, the window's last partial block as filter steps)
+    against the step-by-step filter behind the host assembly, 2 and 3 assets, window lengths
+    hitting each middle-block case."""
+    from copula_var import synthetic, tables
+    c = synthetic.baseline_configs()[cfg_no].with_(T=T, n_in=n_in, k=k)
+    rets = synthetic.simulate_returns(c)
+    _, _, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
+    (fbs, pi), uvs, _ = tables.msm_integration_params(centred, c.n_in, c.msm_params, c.k, c.num_points)
+    mt, uvs_d, _ = _device_tables(centred[:-1], c.n_in, c.k, c.msm_params)
+    np.testing.assert_array_equal(uvs_d, uvs)
+    np.testing.assert_allclose(mt.fbs.cpu().numpy(), fbs, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(mt.pi.cpu().numpy(), pi, rtol=1e-12, atol=1e-300)

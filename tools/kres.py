@@ -17,7 +17,7 @@ for line in sys.stdin:
 for r in rows:
     if flt in r["name"]:
         dem = subprocess.run(["c++filt", r["name"]], capture_output=True, text=True).stdout.strip()
-        dem = re.sub(r"\(.*", "", dem)
+        dem = re.sub(r"\(.*", "", dem.replace("(anonymous namespace)::", ""))
         print(f"{dem:60s} vgpr {r.get('VGPRs')} agpr {r.get('AGPRs')} sgpr {r.get('SGPRs')} "
               f"vspill {r.get('VGPRs Spill')} sspill {r.get('SGPRs Spill')} occ {r.get('Occupancy [waves/SIMD]')} "
               f"lds {r.get('LDS Size [bytes/block]')}")
