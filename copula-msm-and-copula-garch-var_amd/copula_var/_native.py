@@ -76,6 +76,7 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_plan_kernel_time": (i32, [v, i32, C.POINTER(d), _ip]),
         "cvq_plan_debug_stamps": (i32, [v, v, i64]),
         "cvq_plan_debug_nodes": (i32, [v, v, i64, v]),
+        "cvq_plan_debug_cuts": (i32, [v, v, i64, v]),
         "cvq_plan_count_nodes": (i32, [v, i32]),
         "cvq_plan_nodes_evaluated": (i32, [v, C.POINTER(i64)]),
         "cvq_set_dates": (i32, [v, i64, v, v, i32]),

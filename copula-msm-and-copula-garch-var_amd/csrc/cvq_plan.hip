@@ -186,6 +186,7 @@ struct cvq_plan {
     bool sweep_ok = false;       // SWEEP usable for the cached solve arguments (levels ordered)
     int layout = 0;              // SORTED node-word layout (sorted_pack)
     int fixpos[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<int> hcuts;      // solve-order segment ends (ensure_sorted_tree; cvq_plan_debug_cuts)
     double tree_key[7] = {0, 0, 0, 0, 0, 0, 0};
     bool tree_valid = false;
     long long capStamps = 0;
@@ -508,6 +509,7 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
     cuts.push_back(G);
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    p->hcuts = cuts;
     const int bpos[4][2] = {{p->fixpos[4], p->fixpos[1]}, {p->fixpos[1], p->fixpos[2]},
                             {p->fixpos[3], p->fixpos[5]}, {p->fixpos[2], p->fixpos[3]}};
     std::vector<uint32_t> pidx(p->hidx);
@@ -535,6 +537,70 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
             pidx[q] = p->hidx[ord[q - c0].second];
             pvs[q] = vs[ord[q - c0].second];
         }
+    }
+    // Bank-aware order (SORTED, 2-D): the solve's range sums read position q in lane q mod 64
+    // (k_sorted aligns every range to 64), so inside each freely ordered segment the host picks,
+    // position by position, the node whose two 16-B LDS records add the fewest bank-slot
+    // conflicts to its ds_read_b128 lane group (MI355X_MICROARCH.md §LDS) among the next 64 of
+    // the row-major order (tools/lds_sim.py: 9-12 LDS cycles per record read -> see DESIGN.md).
+    static const bool bank_order = !getenv("CVQ_SORT_BANK") || atoi(getenv("CVQ_SORT_BANK")) != 0;   // A/B
+    if (bank_order && p->strategy == CVQ_STRATEGY_SORTED && lay == kLay2) {
+        auto group_of = [](int l) {                            // ds_read_b128 lane groups
+            const int h = l >> 5, m = l & 31;
+            const int g = (m < 4 || (m >= 12 && m < 16) || (m >= 20 && m < 28)) ? 0 : 1;
+            return 2 * h + g;
+        };
+        std::vector<uint32_t> nidx(pidx.begin(), pidx.begin() + G);
+        std::vector<double> nvs(pvs.begin(), pvs.begin() + G);
+        // per segment: a window of the next <= 64 candidates (row-major stream position `next`)
+        struct Seg { int c0, c1, next; bool keep; std::vector<int> win; };
+        std::vector<Seg> segs;
+        for (size_t k = 0; k + 1 < cuts.size(); ++k) {
+            const int c0 = cuts[k], c1 = std::min(cuts[k + 1], G);
+            if (c1 <= c0) continue;
+            bool searchable = false;
+            for (int b = 0; b < 4; ++b) searchable |= c1 - c0 > tcap && c0 >= bpos[b][0] && c1 <= bpos[b][1];
+            segs.push_back({c0, c1, c0, searchable || c1 - c0 < 2, {}});
+        }
+        size_t si = 0;
+        for (int blk = 0; blk < G; blk += 64) {
+            std::vector<uint32_t> ra[4][16], ca[4][16];        // distinct record addresses per group / slot
+            for (int q = blk; q < std::min(blk + 64, G); ++q) {
+                while (segs[si].c1 <= q) ++si;
+                Seg& sg = segs[si];
+                const int g = group_of(q & 63);
+                uint32_t c;
+                double v;
+                if (sg.keep) {
+                    c = pidx[q];
+                    v = pvs[q];
+                } else {
+                    while ((int)sg.win.size() < 64 && sg.next < sg.c1) sg.win.push_back(sg.next++);
+                    int best = 0, bscore = 1 << 30;
+                    for (int k = 0; k < (int)sg.win.size(); ++k) {
+                        const uint32_t w = pidx[sg.win[k]];
+                        const uint32_t a1 = w & 0xFFFFu, a2 = w >> 16;
+                        const std::vector<uint32_t>& v1 = ra[g][(a1 >> 4) & 15];
+                        const std::vector<uint32_t>& v2 = ca[g][(a2 >> 4) & 15];
+                        const int sc = (std::find(v1.begin(), v1.end(), a1) != v1.end() ? 0 : (int)v1.size()) +
+                                       (std::find(v2.begin(), v2.end(), a2) != v2.end() ? 0 : (int)v2.size());
+                        if (sc < bscore) { bscore = sc; best = k; if (sc == 0) break; }
+                    }
+                    const int src = sg.win[best];
+                    sg.win.erase(sg.win.begin() + best);
+                    c = pidx[src];
+                    v = pvs[src];
+                }
+                nidx[q] = c;
+                nvs[q] = v;
+                std::vector<uint32_t>& v1 = ra[g][((c & 0xFFFFu) >> 4) & 15];
+                std::vector<uint32_t>& v2 = ca[g][((c >> 16) >> 4) & 15];
+                if (std::find(v1.begin(), v1.end(), c & 0xFFFFu) == v1.end()) v1.push_back(c & 0xFFFFu);
+                if (std::find(v2.begin(), v2.end(), c >> 16) == v2.end()) v2.push_back(c >> 16);
+            }
+        }
+        std::copy(nidx.begin(), nidx.end(), pidx.begin());
+        std::copy(nvs.begin(), nvs.end(), pvs.begin());
     }
     if (p->strategy == CVQ_STRATEGY_SWEEP && (lay == kLay2 || lay == kLay2W)) {
         // SWEEP's lanes read positions a chunk apart, not consecutive ones: inside each segment of
@@ -609,7 +675,7 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
         greedy(p->fixpos[0], p->fixpos[3]);
         greedy(p->fixpos[3], std::max(p->fixpos[5], p->fixpos[3]));
     }
-    pidx.resize(((pidx.size() + 3) & ~(size_t)3) + 4, 0u);
+    pidx.resize(((pidx.size() + 3) & ~(size_t)3) + kSortIdxPad, 0u);
     if (int rc = dev_alloc(&p->d_pidx, pidx.size())) return rc;
     if (int rc = dev_alloc(&p->d_pvs, std::max<size_t>(pvs.size(), 1))) return rc;
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pidx, pidx.data(), pidx.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
@@ -1307,7 +1373,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         build_sorted_nodes(p->hx, S, kmax, p->layout, p->hvs, idx);
         const size_t nv = idx.size();
         p->hidx = idx;
-        idx.resize(((nv + 3) & ~(size_t)3) + 4, 0u);        // SWEEP's 16-B loads read up to 4 words ahead
+        idx.resize(((nv + 3) & ~(size_t)3) + kSortIdxPad, 0u);   // SWEEP / range-sum loads past the end
         if ((rc = dev_alloc(&p->d_sidx, idx.size())) || (rc = dev_alloc(&p->d_svs, nv))) {
             cvq_plan_destroy(p);
             return rc;
@@ -1432,6 +1498,14 @@ int32_t cvq_plan_debug_nodes(cvq_plan* p, uint32_t* host, int64_t count, int32_t
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     CVQ_HIP_CHECK(hipMemcpy(host, p->d_pidx, count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (fix) for (int e = 0; e < 6; ++e) fix[e] = p->fixpos[e];
+    return CVQ_OK;
+}
+
+int32_t cvq_plan_debug_cuts(cvq_plan* p, int32_t* host, int64_t cap, int32_t* count) {
+    CVQ_REQUIRE(p != nullptr && count != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(p->tree_valid, CVQ_ERR_STATE, "no solve-order node list (a SORTED plan builds it at its first solve)");
+    *count = (int32_t)p->hcuts.size();
+    if (host) for (int64_t k = 0; k < std::min<int64_t>(cap, (int64_t)p->hcuts.size()); ++k) host[k] = p->hcuts[k];
     return CVQ_OK;
 }
 

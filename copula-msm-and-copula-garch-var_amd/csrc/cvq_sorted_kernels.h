@@ -49,6 +49,12 @@ constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisec
 #ifndef CVQ_SORT_ILP
 #define CVQ_SORT_ILP 4
 #endif
+#ifndef CVQ_SORT_PREFETCH
+#define CVQ_SORT_PREFETCH 1        // range sums load the next round's node words a round ahead
+#endif
+// zero words after the node lists: a range sum's prefetch reads up to one round (kSortIlp x the
+// widest workgroup) past its range, SWEEP's 16-B loads up to 4 words
+constexpr int kSortIdxPad = CVQ_SORT_ILP * 1024;
 constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
 
 // SWEEP (2-D): boundary list capacity per pass (LDS, double-buffered), the depth of the
@@ -287,7 +293,12 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     };
     long long nodes = 0;                           // nodes evaluated (thread 0, stamps only)
     stamp(0);
-    if (stamps && tid == 0) stamps[25] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && tid == 0) {
+        stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+        // placement: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of this workgroup's first wave
+        stamps[27] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                     ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+    }
     if (tid == 0) flags = 0;
     __syncthreads();
     // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
@@ -407,9 +418,12 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 r[2] = sf * (kq * S.Ri[3] * (z * z));
             }
             r[3] = 0.0;
-        } else {                                           // Student: z and scale; Plackett: u and scale
-            const double sc = (ax == 0 && COP == CVQ_STUDENT ? S.term1 : 1.0) * B *
-                              (ax == 0 && DIM == 3 ? arest : w);
+        } else if constexpr (COP == CVQ_PLACKETT) {       // rec0 = (-2 u, theta s), rec2 = ((theta - 1) v, s)
+            double* r = ax == 0 ? fr0 + 2 * i : fr2 + 2 * i;
+            r[0] = ax == 0 ? -2.0 * z : (S.theta - 1.0) * z;
+            r[1] = (ax == 0 ? S.theta : 1.0) * (B * w);
+        } else {                                           // Student: z and scale
+            const double sc = (ax == 0 ? S.term1 : 1.0) * B * (ax == 0 && DIM == 3 ? arest : w);
             double* r = ax == 0 ? fr0 + 2 * i : ax == DIM - 1 ? fr2 + 2 * i : fr1 + R1 * i;
             r[0] = z;
             r[1] = sc;
@@ -445,6 +459,21 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         else return lds_at(lds_base(fr2) + 16 * (c >> 17));
     };
     constexpr double kFoldClamp = pow2_constexpr(2000 / (PM > 0 ? PM : 2000));
+    // Plackett node (plackett.py:66-69, Q11) from the records (-2 u, theta s0), (a1 v, s2),
+    // a1 = theta - 1: P = 1 + a1 (u + v), num / theta = 1 + a1 (u + v - 2 u v) = P + (-2 u)(a1 v),
+    // denominator (P (theta + 1 - P))^2 -- 14 FP64 operations and one reciprocal a node
+    const double pl_h = -0.5 * (S.theta - 1.0), pl_k = S.theta + 1.0;
+    auto plackett = [&](const double2 A, const double2 C) -> double {
+        const double P = fma(pl_h, A.x, 1.0 + C.x);
+        const double num = fma(A.x, C.x, P);
+        const double d = P * (pl_k - P);
+        const double den = d * d;
+        double y = __builtin_amdgcn_rcp(den);
+        y = fma(y, fma(-den, y, 1.0), y);
+        y = fma(y, fma(-den, y, 1.0), y);
+        y = den == 0.0 ? __builtin_inf() : y;             // num / 0 as IEEE division gives it (num * inf)
+        return (num * y) * (A.y * C.y);
+    };
     // 2-D node from its two 16-B records (kLay2): the sweep issues a round's LDS reads first
     auto node2 = [&](const double2 A, const double2 C) -> double {
         if constexpr (COP == CVQ_GAUSSIAN) {
@@ -453,16 +482,7 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
             const double b = fma(A.x, fma(a00, A.x, k02 * C.x), fma(a22 * C.x, C.x, 1.0));
             return (A.y * C.y) * pow_fast<PM>(b, S.node_m, S.node_ex);
         } else {
-            const double th = S.theta, a1 = th - 1.0, u = A.x, v = C.x, s2 = u + v;
-            const double num = th * fma(a1, fma(-2.0 * u, v, s2), 1.0);
-            const double d = fma(a1, s2, 1.0) * fma(-a1, s2, 1.0 + a1);
-            const double den = d * d;
-            double y = __builtin_amdgcn_rcp(den);
-            y = fma(y, fma(-den, y, 1.0), y);
-            y = fma(y, fma(-den, y, 1.0), y);
-            const double c0 = den == 0.0 ? (num == 0.0 ? __builtin_nan("") : __builtin_copysign(__builtin_inf(), num))
-                                         : num * y;
-            return c0 * (A.y * C.y);
+            return plackett(A, C);
         }
     };
     auto node_fast = [&](uint32_t c) -> double {
@@ -498,18 +518,8 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 sc = (A.y * Bv.y) * C.y;
             }
             return sc * pow_fast<PM>(b, S.node_m, S.node_ex);
-        } else {                                           // Plackett (plackett.py:66-69, Q11), 2-D
-            const double th = S.theta, a1 = th - 1.0, u = A.x, v = C.x, s2 = u + v;
-            const double num = th * fma(a1, fma(-2.0 * u, v, s2), 1.0);
-            const double d = fma(a1, s2, 1.0) * fma(-a1, s2, 1.0 + a1);
-            const double den = d * d;
-            double y = __builtin_amdgcn_rcp(den);
-            y = fma(y, fma(-den, y, 1.0), y);
-            y = fma(y, fma(-den, y, 1.0), y);
-            // num / 0 as IEEE division gives it (the Newton steps would give NaN)
-            const double c0 = den == 0.0 ? (num == 0.0 ? __builtin_nan("") : __builtin_copysign(__builtin_inf(), num))
-                                         : num * y;
-            return c0 * (A.y * C.y);
+        } else {                                           // Plackett, 2-D
+            return plackett(A, C);
         }
     };
     auto node_generic = [&](uint32_t c) -> double {
@@ -546,14 +556,71 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         else ctx = make_row<COP, 3>(S, zg[i0], zg[n + i1], Bg[i0] * Bg[n + i1]);
         return node_value<COP, MSM, DIM>(S, ctx, zi, Bi, W);
     };
-    // sum of the nodes at sorted positions [p0, p1), strided over the workgroup; the
-    // last (partial) round is predicated so its index loads are in flight together
+    // sum of the nodes at sorted positions [p0, p1), strided over the workgroup: the rounds start
+    // at p0 rounded down to 64, so position q is always read by lane q mod 64 (the plan's
+    // bank-aware order, ensure_sorted_tree); the first round is predicated below p0, the last
+    // (partial) one above p1, so their index loads are in flight together
     auto range_sum = [&](int p0, int p1) -> double {
         double acc[kSortIlp];
 #pragma unroll
         for (int u = 0; u < kSortIlp; ++u) acc[u] = 0.0;
-        int p = p0 + tid;
-        if (fast) {
+        int p = (p0 & ~63) + tid;
+        if (fast && p0 < p1) {
+#if CVQ_SORT_PREFETCH
+            // the next round's node words are loaded before this round's nodes are evaluated (a
+            // few dates per CU leave too few waves to cover the L2 latency of unpipelined loads).
+            // Loads run up to a round past p1 (the lists carry kSortIdxPad zero words) and from
+            // p0 rounded down to 64 (>= 0): unconditional, the first and last rounds select their
+            // out-of-range nodes away
+            uint32_t cn[kSortIlp];
+            const uint32_t* ip = G.idx + p;                // this thread's words of the next round
+            {                                              // first round: positions below p0 masked
+                uint32_t c[kSortIlp];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) c[u] = ip[u * NT];
+                ip += kSortIlp * NT;
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) cn[u] = ip[u * NT];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) {
+                    const int q = p + u * NT;
+                    const double v = node_fast(c[u]);
+                    acc[u] += (q >= p0 && q < p1) ? v : 0.0;
+                }
+                p += kSortIlp * NT;
+            }
+            for (; p + (kSortIlp - 1) * NT < p1; p += kSortIlp * NT) {   // full rounds
+                uint32_t c[kSortIlp];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) c[u] = cn[u];
+                ip += kSortIlp * NT;
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) cn[u] = ip[u * NT];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(c[u]);
+            }
+            if (p < p1) {                                  // last round: positions from p1 on masked
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) {
+                    const double v = node_fast(cn[u]);
+                    acc[u] += p + u * NT < p1 ? v : 0.0;
+                }
+            }
+#else
+            {                                              // first round: positions below p0 masked
+                uint32_t c[kSortIlp];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) {
+                    const int q = p + u * NT;
+                    c[u] = (q >= p0 && q < p1) ? G.idx[q] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) {
+                    const int q = p + u * NT;
+                    if (q >= p0 && q < p1) acc[u] += node_fast(c[u]);
+                }
+                p += kSortIlp * NT;
+            }
             for (; p + (kSortIlp - 1) * NT < p1; p += kSortIlp * NT) {
                 uint32_t c[kSortIlp];
 #pragma unroll
@@ -569,8 +636,9 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 for (int u = 0; u < kSortIlp; ++u)
                     if (p + u * NT < p1) acc[u] += node_fast(c[u]);
             }
+#endif
         } else {
-            for (; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
+            for (p = p0 + tid; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
         }
 #pragma unroll
         for (int h = 1; h < kSortIlp; h <<= 1)

@@ -122,6 +122,9 @@ int32_t cvq_plan_debug_stamps(cvq_plan* plan, uint64_t* host, int64_t count);
    nodes; the LDS byte offsets of their records, cvq_sorted_kernels.h sorted_pack) and, when
    fix != NULL, the sorted positions of the six fixed levels of the last solve's arguments. */
 int32_t cvq_plan_debug_nodes(cvq_plan* plan, uint32_t* host, int64_t count, int32_t* fix);
+/* Diagnostics: the ends of the solve-order segments (positions the solve's range sums start or
+ * end at; inside one the node order is free).  Writes min(cap, *count) of them. */
+int32_t cvq_plan_debug_cuts(cvq_plan* plan, int32_t* host, int64_t cap, int32_t* count);
 /* Measurement aid (bench.py's FP64 roofline basis): with cvq_plan_count_nodes(plan, 1)
  * the following COMPACT / SORTED / SWEEP solves record how many quadrature nodes each
  * date evaluated (the phase-stamp buffer: slower, never in a timed run);
