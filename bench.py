@@ -168,6 +168,8 @@ def main():
                 shardeds.append(device_sharded_var(p, args, T_total, dev, group=grp))
     plan = plans[0]
 
+    local_only = [False]                              # sharded: time this rank's local solve alone
+
     def step_fn(k):
         with torch.cuda.stream(streams[k]):
             # pi = outer product of the per-asset forecasts (compute_forecast_combinations), so the
@@ -175,6 +177,8 @@ def main():
             plans[k].set_dates_device(per, d_a.data_ptr(), b_ptr, fast=fast_ok)   # forces tables recompute
             if not sharded:
                 plans[k].solve_device(args, vars_[k].data_ptr())
+            elif local_only[0]:
+                shardeds[k].solve_local()
             else:
                 shardeds[k].solve(check=False)
 
@@ -240,6 +244,16 @@ def main():
     single = {"value": T_total * a.steps / el1, "unit": "VaR-dates/s", "ms_per_step": el1 / a.steps * 1e3,
               "inflight": 1, "steps": a.steps,
               "scope": "one calc_var-equivalent solve per step (utils/calc_var_class.py:109-175), tables resident"}
+    if sharded and a.single:
+        # the step's two parts: every rank's local solve of its block (max over ranks), and the
+        # rest -- the one all-gather of the packed blocks + the finalize
+        local_only[0] = True
+        el_loc, _ = timed(1, a.steps, a.warmup)
+        local_only[0] = False
+        single["local_solve_ms"] = el_loc / a.steps * 1e3
+        single["allgather_finalize_ms"] = max(single["ms_per_step"] - single["local_solve_ms"], 0.0)
+        single["split_note"] = ("local_solve_ms: the same one-batch leg without the exchange (barrier + synchronize "
+                                "around K steps, max over ranks); allgather_finalize_ms: ms_per_step minus it")
 
     # roofline of the dominant kernel.  COMPACT / SORTED / SWEEP: the single-solve leg's event
     # bracket / K.  Otherwise (several kernels per step): one batch at a time with HIP events

@@ -77,6 +77,10 @@ class ShardedVaR:
         self.hdr.zero_()
         self.var = torch.empty(self.T_total, dtype=torch.float64, device=device)
 
+    def solve_local(self) -> None:
+        """This rank's part of solve() alone: its block's local solve, no exchange (timing)."""
+        self._local(self.hdr, self.snaps)
+
     def solve(self, check: bool = True) -> torch.Tensor:
         """Full VaR vector on every rank.  check: verify convergence within the
         bisection budget after the finalize (synchronises; the status is global, from

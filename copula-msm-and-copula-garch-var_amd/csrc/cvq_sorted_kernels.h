@@ -461,7 +461,9 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     constexpr double kFoldClamp = pow2_constexpr(2000 / (PM > 0 ? PM : 2000));
     // Plackett node (plackett.py:66-69, Q11) from the records (-2 u, theta s0), (a1 v, s2),
     // a1 = theta - 1: P = 1 + a1 (u + v), num / theta = 1 + a1 (u + v - 2 u v) = P + (-2 u)(a1 v),
-    // denominator (P (theta + 1 - P))^2 -- 14 FP64 operations and one reciprocal a node
+    // denominator (P (theta + 1 - P))^2 -- 12 FP64 operations and one reciprocal a node: v_rcp_f64
+    // (2^-24.4) and one Newton step, 2.2e-15 relative (profiles/r04f/rcp_probe.txt), as pow_fast's
+    // Student reciprocal (the VaR is unchanged by 1e-8 relative node noise)
     const double pl_h = -0.5 * (S.theta - 1.0), pl_k = S.theta + 1.0;
     auto plackett = [&](const double2 A, const double2 C) -> double {
         const double P = fma(pl_h, A.x, 1.0 + C.x);
@@ -469,7 +471,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         const double d = P * (pl_k - P);
         const double den = d * d;
         double y = __builtin_amdgcn_rcp(den);
-        y = fma(y, fma(-den, y, 1.0), y);
         y = fma(y, fma(-den, y, 1.0), y);
         y = den == 0.0 ? __builtin_inf() : y;             // num / 0 as IEEE division gives it (num * inf)
         return (num * y) * (A.y * C.y);
@@ -589,15 +590,29 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 }
                 p += kSortIlp * NT;
             }
-            for (; p + (kSortIlp - 1) * NT < p1; p += kSortIlp * NT) {   // full rounds
-                uint32_t c[kSortIlp];
+            uint32_t cm[kSortIlp];
+            // full rounds in pairs, the word buffers alternating (no register copies)
+            for (; p + (2 * kSortIlp - 1) * NT < p1; p += 2 * kSortIlp * NT) {
+                ip += kSortIlp * NT;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) c[u] = cn[u];
+                for (int u = 0; u < kSortIlp; ++u) cm[u] = ip[u * NT];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cn[u]);
                 ip += kSortIlp * NT;
 #pragma unroll
                 for (int u = 0; u < kSortIlp; ++u) cn[u] = ip[u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(c[u]);
+                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cm[u]);
+            }
+            if (p + (kSortIlp - 1) * NT < p1) {            // an odd full round
+                ip += kSortIlp * NT;
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) cm[u] = ip[u * NT];
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cn[u]);
+#pragma unroll
+                for (int u = 0; u < kSortIlp; ++u) cn[u] = cm[u];
+                p += kSortIlp * NT;
             }
             if (p < p1) {                                  // last round: positions from p1 on masked
 #pragma unroll

@@ -94,6 +94,7 @@ void sorted_launch_nt(const SortedLaunch& L) {
 }
 
 // the wider instances (cvq_sorted_inst.hip)
+void sorted_slice_384(const SortedLaunch& L);
 void sorted_slice_512(const SortedLaunch& L);
 void sorted_slice_1024(const SortedLaunch& L);
 

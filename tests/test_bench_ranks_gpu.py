@@ -46,10 +46,14 @@ COMMON = ["--steps", "3", "--warmup", "1", "--cpu-baseline", "0", "--e2e", "0", 
 def test_two_ranks_weak_and_strong_match_one_rank():
     one = _bench(COMMON + ["--dates-per-gpu", "240"], 1)
     weak = _bench(COMMON + ["--dates-per-gpu", "120"], 2)           # 2 x 120 dates of the same series
-    strong = _bench(COMMON + ["--global-dates", "240"], 2)          # 240 dates split 120 / 120
+    strong = _bench(COMMON + ["--global-dates", "240", "--single", "1"], 2)   # 240 dates split 120 / 120
     assert one["var_nan"] == 0
     for r in (weak, strong):
         assert r["n_gpus"] == 2 and r["config"]["global_dates"] == 240
         assert r["var_checksum"] == one["var_checksum"], (r["var_checksum"], one["var_checksum"])
         assert r["value"] > 0
     assert weak["scaling"] == "weak" and strong["scaling"] == "strong"
+    # the one-batch step split into the ranks' local solve and the all-gather + finalize
+    ss = strong["single_solve"]
+    assert 0 < ss["local_solve_ms"] <= ss["ms_per_step"] * 1.5
+    assert ss["allgather_finalize_ms"] >= 0.0

@@ -1,4 +1,4 @@
-"""SORTED at 256, 512 and 1024 threads per date (cvq_sorted.hip sorted_threads).
+"""SORTED at 256, 384, 512 and 1024 threads per date (cvq_sorted.hip sorted_threads).
 
 A strong-scaling block of a few hundred dates per GPU takes the wider workgroups (the
 launch is latency bound there); a full batch takes 256.  The width changes only how a
@@ -14,7 +14,7 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-WIDTHS = ["256", "512", "1024"]
+WIDTHS = ["256", "384", "512", "1024"]
 
 
 @pytest.fixture(scope="module", autouse=True)

@@ -9,9 +9,9 @@ out=../build_variants/$name
 mkdir -p $out
 CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function"
 $CXX "$@" -c csrc/cvq_sorted.hip -o $out/cvq_sorted.o &
-for w in 512 1024; do
+for w in 384 512 1024; do
   $CXX "$@" -DCVQ_SORT_SLICE_$w -c csrc/cvq_sorted_inst.hip -o $out/cvq_si_$w.o &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libcvq.so build/cvq_plan.o build/cvq_forecast.o \
-    build/cvq_compact.o build/cvq_ci_*.o $out/cvq_sorted.o $out/cvq_si_512.o $out/cvq_si_1024.o
+    build/cvq_compact.o build/cvq_ci_*.o $out/cvq_sorted.o $out/cvq_si_384.o $out/cvq_si_512.o $out/cvq_si_1024.o
