@@ -90,6 +90,7 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_solve_local": (i32, [v, C.POINTER(CvqSolveArgs), v, v]),
         "cvq_solve_finalize": (i32, [v, C.POINTER(CvqSolveArgs), v, i32, v, i64, i64, v]),
         "cvq_msm_filter": (i32, [i32, i32, d, d, d, d, v, i64, i64, v, i32]),
+        "cvq_msm_marginals": (i32, [i32, i32, d, d, d, d, v, i64, v, v, i32]),
         "cvq_msm_tables_scratch": (i32, [i32, i32, i64, i64, C.POINTER(C.c_int64)]),
         "cvq_msm_tables": (i32, [i32, v, i32, i32, v, v, i32, v, i64, i64, v, v, v]),
         "cvq_msm_tables_status": (i32, [v, i32, i32, i64, i64, v]),

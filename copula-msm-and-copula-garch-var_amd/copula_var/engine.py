@@ -354,6 +354,17 @@ def msm_filter(returns_c, n_in: int, k: int, m0: float, sig: float, b: float, ga
     return out
 
 
+def msm_marginals(returns, k: int, m0: float, sig: float, b: float, gamma: float, device: int = 0):
+    """In-sample MSM marginals and densities of one return series on the device
+    (cvq_msm_marginals; calc_marginals.py:7-30): two arrays of length N - 1."""
+    r = N.f64(returns)
+    m = np.empty(r.size - 1)
+    d = np.empty(r.size - 1)
+    N.check(N.lib().cvq_msm_marginals(device, k, m0, sig, b, gamma, N.ptr(r), r.size, N.ptr(m), N.ptr(d),
+                                      N.MEM_HOST), "cvq_msm_marginals")
+    return m, d
+
+
 class MsmTables:
     """Device-resident MSM forecast stage (cvq_msm_tables): every asset's rolling-window
     Hamilton filters, the per-state collapse onto unique vols and the forecast

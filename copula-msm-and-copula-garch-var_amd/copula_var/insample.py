@@ -1,10 +1,11 @@
 """In-sample marginals and densities that feed the copula fit
 (calculate_marginals_and_densities_in_sample of the three model adapters).
 
-One pass over the N in-sample returns per asset, once per fit: the MSM filtered
-state probabilities and the GARCH variance recursion are O(N * 2^2k) / O(N) host
-loops in numpy (the reference runs them in numba); the UKF state path comes from
-the device filter (cvq_ukf_filter), the kernel the EM fit uses.
+One pass over the N in-sample returns per asset, once per fit: the MSM marginals come
+from the device filter (cvq_msm_marginals; msm_marginals_densities is its host
+restatement, kept for the CPU tests), the UKF state path from the device filter
+(cvq_ukf_filter, the kernel the EM fit uses); the GARCH variance recursion is an O(N)
+host loop.
 """
 from __future__ import annotations
 
@@ -66,6 +67,16 @@ def msm_marginals_densities(returns, k, m0, sig, b, gamma):
     marginals = np.sum(probs[1:, :] * cond_marg[:-1, :], axis=1)
     densities = np.sum(probs[1:, :] * cond[:-1, :], axis=1)
     return marginals, densities, vol
+
+
+def msm_marginals_densities_device(returns, k, m0, sig, b, gamma, device: int = 0):
+    """msm_marginals_densities on the device (cvq_msm_marginals: one Hamilton-filter pass,
+    the state sums per step in the same kernel); the vol states from the host transition
+    (calc_prob.py:103-108, exact)."""
+    m, d = engine.msm_marginals(returns, k, m0, sig, b, gamma, device)
+    _, M = msm_transition(k, m0, b, gamma)
+    vol = np.array([np.sqrt(np.prod(M[i])) * sig for i in range(M.shape[0])])
+    return m, d, vol
 
 
 def garch_eps(returns, omega, alpha, beta, epsilon=1e-7):

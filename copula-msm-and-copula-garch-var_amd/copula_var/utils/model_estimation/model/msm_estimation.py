@@ -47,14 +47,16 @@ class MSMEstimation(VaRCalculationMethod):
     def calculate_marginals_and_densities_in_sample(in_sample_dict, in_sample_params, k):
         """msm_estimation.py:55-120: per ticker (cached under (ticker, 'marginals_k'))
         the filtered-probability-weighted normal cdf / pdf of the in-sample returns
-        (calc_marginals.py:7-30), stacked (N-1, dim), and the 2**k vol states."""
+        (calc_marginals.py:7-30; one device filter pass, cvq_msm_marginals), stacked
+        (N-1, dim), and the 2**k vol states."""
         marg, dens, vs = [], [], []
         for ticker, params in in_sample_params.items():
             key = (ticker, f"marginals_{k}")
             if key not in SharedCacheCopulaMSMVaR.cache:
                 op = params["optimal_params"]
-                m, d, v = insample.msm_marginals_densities(np.asarray(in_sample_dict[ticker], dtype=np.float64), k,
-                                                           op["m_0"], op["sig"], op["b"], op["gamma"])
+                m, d, v = insample.msm_marginals_densities_device(
+                    np.asarray(in_sample_dict[ticker], dtype=np.float64), k, op["m_0"], op["sig"], op["b"],
+                    op["gamma"], MSMEstimation.device)
                 SharedCacheCopulaMSMVaR.cache[key] = {"marginals": m, "densities": d, "vol_states": v}
             c = SharedCacheCopulaMSMVaR.cache[key]
             marg.append(np.asarray(c["marginals"]).reshape(-1, 1))

@@ -1157,6 +1157,61 @@ __global__ __launch_bounds__(256) void k_msm_loglik(const MsmParams* __restrict_
     if (active && lane_q == 0) out[bi] = dead ? -__builtin_huge_val() : LL;
 }
 
+// scipy.special.ndtr (norm.cdf, calc_prob.py:128): the erf form near 0, the erfc tail beyond
+// |x| / sqrt 2 >= 1 / sqrt 2, as cephes' ndtr evaluates it (relative accuracy in both tails).
+__device__ __forceinline__ double ndtr_dev(double a) {
+    const double x = a * 0.70710678118654752440, z = fabs(x);
+    if (z < 0.70710678118654752440) return 0.5 + 0.5 * erf(x);
+    const double y = 0.5 * erfc(z);
+    return x > 0.0 ? 1.0 - y : y;
+}
+
+// In-sample MSM marginals and densities (calc_marginals.py:7-30, the copula fit's inputs):
+// the filtered state probabilities of every step (calc_prob.py:51-69, normalised by IEEE
+// division as the reference does) weighted by the conditional CDF / pdf of the PREVIOUS return,
+//   marg[i - 1] = sum_s prob[i][s] ndtr(r[i-1] / vs_s),  dens[i - 1] = sum_s prob[i][s] pdf(r[i-1]; vs_s),
+// i = 1 .. N - 1 (state_prob_t[1:] * cond_marg_vect[:-1]).  One quad (L lanes) per series
+// (blockIdx.x): the steps are a dependent chain; the state sums reduce by quad DPP.
+template <int K>
+__global__ void k_msm_marginals(MsmParams P, const double* __restrict__ r, long long N, double* __restrict__ marg,
+                                double* __restrict__ dens, int* err) {
+    constexpr int S = Quad<K>::S, L = Quad<K>::L, SL = Quad<K>::SL;
+    const int lane_q = threadIdx.x;                    // blockDim.x == L
+    double v[SL], vs[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+        v[j] = 1.0 / S;                                // equi_prob (calc_prob.py:12-13)
+        vs[j] = P.vs[lane_q * SL + j];
+    }
+    bool bad = false;
+    double rprev = 0.0;
+    for (long long i = 0; i < N; ++i) {
+        const double ri = r[i];
+        double cv[SL];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) cv[j] = cond_prob(ri, vs[j]);
+        bool z;
+        msm_step<K, true>(v, cv, P, &z);
+        bad |= z;
+        if (i >= 1) {
+            double pm = 0.0, pd = 0.0;
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                pm += v[j] * ndtr_dev(rprev / vs[j]);
+                pd += v[j] * cond_prob(rprev, vs[j]);
+            }
+            if (L >= 2) { pm += quad_xor<1>(pm); pd += quad_xor<1>(pd); }
+            if (L >= 4) { pm += quad_xor<2>(pm); pd += quad_xor<2>(pd); }
+            if (lane_q == 0) {
+                marg[i - 1] = pm;
+                dens[i - 1] = pd;
+            }
+        }
+        rprev = ri;
+    }
+    if (bad && lane_q == 0) atomicOr(err, 1);
+}
+
 // ----------------------------------------------------------------- GARCH(1,1)
 __global__ void k_garch_forecast(double omega, double alpha, double beta, const double* __restrict__ r,
                                  long long n_in, long long T, double* __restrict__ out) {
@@ -1889,6 +1944,42 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
     hipLaunchKernelGGL(k_msm_cond, dim3((unsigned)((N * S + 255) / 256), 1), dim3(256), 0, 0, P, S, d_r, N, cond.p);
     if ((rc = launch_filter_k(k, P, 1, cond.p, N, n_in, T, d_out, err.p, 0))) return rc;
     if ((rc = finish_out(out, (size_t)T * S, mem, dout))) return rc;
+    int e = 0;
+    CVQ_HIP_CHECK(hipMemcpy(&e, err.p, sizeof(int), hipMemcpyDeviceToHost));
+    CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");
+    return CVQ_OK;
+}
+
+int32_t cvq_msm_marginals(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
+                          const double* returns, int64_t N, double* marg_out, double* dens_out, int32_t mem) {
+    CVQ_REQUIRE(returns && marg_out && dens_out, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
+    CVQ_REQUIRE(N >= 2, CVQ_ERR_INVALID, "N must be >= 2 (the marginals pair step i with return i - 1)");
+    int rc = check_device(device);
+    if (rc) return rc;
+    const MsmParams P = msm_params(k, m0, sigma, b, gamma);
+    DevBuf rin, dm, dd;
+    DevInt err;
+    const double* d_r;
+    double *d_m, *d_d;
+    if ((rc = stage_in(returns, N, mem, rin, &d_r))) return rc;
+    if ((rc = stage_out(marg_out, N - 1, mem, dm, &d_m))) return rc;
+    if ((rc = stage_out(dens_out, N - 1, mem, dd, &d_d))) return rc;
+    CVQ_HIP_CHECK(hipMalloc((void**)&err.p, sizeof(int)));
+    CVQ_HIP_CHECK(hipMemset(err.p, 0, sizeof(int)));
+    const int L = (1 << k) < 4 ? (1 << k) : 4;
+    switch (k) {
+        case 1: hipLaunchKernelGGL(k_msm_marginals<1>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        case 2: hipLaunchKernelGGL(k_msm_marginals<2>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        case 3: hipLaunchKernelGGL(k_msm_marginals<3>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        case 4: hipLaunchKernelGGL(k_msm_marginals<4>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        case 5: hipLaunchKernelGGL(k_msm_marginals<5>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        case 6: hipLaunchKernelGGL(k_msm_marginals<6>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+        default: hipLaunchKernelGGL(k_msm_marginals<7>, dim3(1), dim3(L), 0, 0, P, d_r, N, d_m, d_d, err.p); break;
+    }
+    CVQ_HIP_CHECK(hipGetLastError());
+    if ((rc = finish_out(marg_out, N - 1, mem, dm))) return rc;
+    if ((rc = finish_out(dens_out, N - 1, mem, dd))) return rc;
     int e = 0;
     CVQ_HIP_CHECK(hipMemcpy(&e, err.p, sizeof(int), hipMemcpyDeviceToHost));
     CVQ_REQUIRE(e == 0, CVQ_ERR_NUMERIC, "MSM Bayes update normaliser is 0 (calc_prob.py:64-65)");

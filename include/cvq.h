@@ -214,6 +214,13 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
                        const int32_t* state_map, int32_t q, const double* returns_c, int64_t n_in,
                        int64_t T, double* scratch, double* fbs_out, double* pi_out);
 int32_t cvq_msm_tables_status(double* scratch, int32_t dim, int32_t k, int64_t n_in, int64_t T, void* stream);
+/* In-sample MSM marginals and densities of ONE asset's return series (calc_marginals.py:7-30,
+ * used by MsmEstimation.calculate_marginals_and_densities_in_sample, msm_estimation.py:90-104):
+ * marg_out / dens_out [N - 1] = sum over states of the filtered probabilities of step i
+ * (calc_prob.py:51-69) times norm.cdf / norm.pdf of return i - 1 (calc_prob.py:110-132).
+ * CVQ_ERR_NUMERIC on a zero Bayes normaliser (calc_prob.py:64-65). */
+int32_t cvq_msm_marginals(int32_t device, int32_t k, double m0, double sigma, double b, double gamma,
+                          const double* returns, int64_t N, double* marg_out, double* dens_out, int32_t mem);
 /* GARCH(1,1) compute_forecast (garch_estimation.py:190-231 -> garch/forecast.py:5-19).
  * out [T] = sigma forecast per window. */
 int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double beta,

@@ -79,7 +79,7 @@ def test_copula_parameter_packing():
 def test_insample_stages_use_the_caches_then_the_device():
     """model_params_insample: the reference's cache first (msm_estimation.py:35-38); a miss
     runs the device-batched optimiser, which fails loudly without a GPU.  The in-sample
-    marginals (host filter) are cached under the reference's key."""
+    marginals (device filter, likewise) are cached under the reference's key."""
     from copula_var import _native as N
     from copula_var.utils.factory import ValueAtRiskCalculationFactory as F
     from copula_var.utils.calc_var_ABC import SharedCacheCopulaMSMVaR
@@ -91,6 +91,11 @@ def test_insample_stages_use_the_caches_then_the_device():
     SharedCacheCopulaMSMVaR.cache[("A", 4)] = {"optimal_params": {"m_0": 0.45, "sig": 1.2, "b": 3.0, "gamma": 0.3}}
     r = np.linspace(-2, 2, 40)
     got = c.model_params_insample({"A": r}, k=4)
+    if not _gpu():                                   # the device filter (cvq_msm_marginals) fails loudly
+        with pytest.raises(N.NativeError):
+            c.calculate_marginals_and_densities_in_sample({"A": r}, got, k=4)
+        SharedCacheCopulaMSMVaR.cache.clear()
+        return
     m, d, vsa = c.calculate_marginals_and_densities_in_sample({"A": r}, got, k=4)
     assert vsa.shape == (1, 16) and m.shape == d.shape == (39, 1)
     assert np.all((m > 0) & (m < 1)) and np.all(d > 0)

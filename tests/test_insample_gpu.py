@@ -22,6 +22,28 @@ def _mr_series(n=400, seed=21):
     return synthetic.simulate_returns(cfg.with_(T=1, n_in=n - 1, seed=seed))
 
 
+def test_msm_marginals_kernel_matches_reference():
+    """cvq_msm_marginals (one device Hamilton-filter pass with the per-step state sums)
+    against calc_marginals / calc_densities run by the reference itself (optim_msm_marg.npz,
+    calc_marginals.py:7-30) and against the host restatement; the filter's transition
+    product sums in another order than the reference's per-row loop, so the bar is
+    relative.  Plus k = 1..6 on a longer series against the host restatement."""
+    from copula_var import engine
+    from copula_var.insample import msm_marginals_densities, msm_marginals_densities_device
+    z = load_golden("optim_msm_marg")
+    for row, mw, dw, vw in zip(z["rows"], z["marginals"], z["densities"], z["vol_states"]):
+        m, d, vol = msm_marginals_densities_device(z["returns"], int(z["k"]), *row)
+        np.testing.assert_array_equal(vol, vw)
+        np.testing.assert_allclose(m, mw, rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(d, dw, rtol=1e-12, atol=1e-300)
+    x = _mr_series(n=1136, seed=5)[:, 0]
+    for k in range(1, 7):
+        m, d = engine.msm_marginals(x, k, 0.6, float(np.std(x)), 2.5, 0.4)
+        mh, dh, _ = msm_marginals_densities(x, k, 0.6, float(np.std(x)), 2.5, 0.4)
+        np.testing.assert_allclose(m, mh, rtol=1e-12, atol=1e-300, err_msg=f"k {k}")
+        np.testing.assert_allclose(d, dh, rtol=1e-12, atol=1e-300, err_msg=f"k {k}")
+
+
 def test_ukf_filter_kernel_matches_oracle():
     from oracle.optim import ukf_filter_batch
     from copula_var import engine
