@@ -28,8 +28,8 @@ int device_cus() {
 // Threads per date (one workgroup each).  A date is a chain of dependent phases (tables, two
 // fixed slabs, ~10 reduced levels, the tail), so a launch with few dates per CU is latency
 // bound: wider workgroups split every range sum over more lanes and shorten the chain.  The
-// widest width whose waves the chip holds at once (T NT / 64 <= CUs x 4 SIMDs x the 2-D
-// kernel's 5 waves per SIMD; 3-D: 4) -- i.e. a strong-scaling block of a few hundred dates per
+// widest width whose waves the chip holds at once (T NT / 64 <= CUs x 4 SIMDs x the kernel's
+// waves per SIMD at that width, sorted_min_waves) -- i.e. a strong-scaling block of a few hundred dates per
 // GPU runs 1024- or 512-thread dates, a full batch 256.  Counting whole workgroups per CU instead
 // (625 dates: 384 threads, every workgroup resident) measured slower than 512 threads with the
 // last ~100 dates starting late (cfg 3 133 vs 116 us, cfg 5 118 vs 103 us; profiles/r04o).
@@ -39,9 +39,8 @@ int sorted_threads(long long T, int dim, bool narrow) {
     const int env = ev ? atoi(ev) : 0;
     if (narrow) return kSortNT;
     if (env == 256 || env == 384 || env == 512 || env == 1024) return env;
-    const long long waves = (long long)device_cus() * 4 * sorted_min_waves(dim);
     for (int nt = 1024; nt > kSortNT; nt >>= 1)
-        if (T * (nt / 64) <= waves) return nt;
+        if (T * (nt / 64) <= (long long)device_cus() * 4 * sorted_min_waves(dim, nt)) return nt;
     return kSortNT;
 }
 

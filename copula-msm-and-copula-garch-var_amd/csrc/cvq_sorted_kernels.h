@@ -56,6 +56,23 @@ constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisec
 // widest workgroup) past its range, SWEEP's 16-B loads up to 4 words
 constexpr int kSortIdxPad = CVQ_SORT_ILP * 1024;
 constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
+#ifndef CVQ_SORT_ILP_GEN
+#define CVQ_SORT_ILP_GEN 1
+#endif
+// nodes in flight per thread of a range sum: the Student nodes with a general power (PM = 0: a
+// fitted nu, exp_node(ex log_node(b))) and the 3-D Student nodes take one at a time, so their
+// temporaries fit the registers of 5 (2-D) / 4 (3-D) waves per SIMD: 4 in flight spilled 158-196
+// / 68-83 VGPRs and ran the nu = 5.364 solves at a third of the speed (cfg 2 3.3 M vs 9.3 M
+// VaR-dates/s), 2 spilled 8-11 and measured 1-3% slower than 1 (profiles/r04r)
+// The 512 / 1024-thread 2-D Student instances (6 waves per SIMD, sorted_min_waves) take
+// CVQ_SORT_ILP_WIDE_ST.
+#ifndef CVQ_SORT_ILP_WIDE_ST
+#define CVQ_SORT_ILP_WIDE_ST 1     // 2 spilled 2 VGPRs at 6 waves per SIMD
+#endif
+__host__ __device__ constexpr int sorted_ilp(int cop, int pm, int dim, int nt = 256) {
+    return (cop == CVQ_STUDENT && (pm == 0 || dim == 3)) ? CVQ_SORT_ILP_GEN
+         : (cop == CVQ_STUDENT && nt >= 512) ? CVQ_SORT_ILP_WIDE_ST : kSortIlp;
+}
 
 // SWEEP (2-D): boundary list capacity per pass (LDS, double-buffered), the depth of the
 // pass-0 subtrees (3 (2^d0 - 1) + 3 <= cap) and of a later pass's subtree (2^d - 1 <= cap).
@@ -238,8 +255,18 @@ inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false, int l
 #ifndef CVQ_SORT_MIN_WAVES3
 #define CVQ_SORT_MIN_WAVES3 4
 #endif
-__host__ __device__ constexpr int sorted_min_waves(int dim) {
-    return dim == 2 ? CVQ_SORT_MIN_WAVES2 : CVQ_SORT_MIN_WAVES3;
+#ifndef CVQ_SORT_MIN_WAVES2W
+#define CVQ_SORT_MIN_WAVES2W 6     // 2-D, 512 / 1024 threads: three 512-thread dates per CU
+#endif
+// waves per SIMD the kernel is compiled for (its register budget).  The wide 2-D instances only
+// run small date blocks (sorted_threads), where residency beats registers: at 6 waves a CU holds
+// three 512-thread dates, so a 625-date block is resident at once (cfg 5: 103 -> 97 us); the
+// 256-thread instances keep 5 (6 cost the full batch 5%, profiles/r04q)
+// (the Student instances with a general power stay at 5: their quantile and node temporaries
+// spill 13-15 VGPRs at 6).  cop / pm = -1: the width rule's generic value.
+__host__ __device__ constexpr int sorted_min_waves(int dim, int nt = 256, int cop = -1, int pm = -1) {
+    return dim == 2 ? ((nt >= 512 && !(cop == CVQ_STUDENT && pm == 0)) ? CVQ_SORT_MIN_WAVES2W : CVQ_SORT_MIN_WAVES2)
+                    : CVQ_SORT_MIN_WAVES3;
 }
 
 // SWEEP (2-D): instead of one strided range sum + one workgroup reduction per
@@ -250,7 +277,7 @@ __host__ __device__ constexpr int sorted_min_waves(int dim) {
 // two prefixes) with no further barrier.  Pass 0 covers (lower, sg1], so r0, the second slab
 // and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes one more.
 template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false>
-__global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(DIM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
+__global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(DIM, NT, COP, PM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
                                                const double* __restrict__ bounds, double* __restrict__ out,
@@ -304,6 +331,7 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
     // axes unrolled so their latencies overlap; kept in registers until the path is chosen
     constexpr int RPT = (sorted_max_n(DIM) + NT - 1) / NT;       // grid indices per thread
+    constexpr int ILP = sorted_ilp(COP, PM, DIM, NT);              // range sums' nodes in flight
     const int q = MSM ? S.q : 1;
     const double* fb = MSM ? a + t * DIM * q : nullptr;     // forecasts_by_states[t] (DIM, q)
     double eA[RPT][DIM], eB[RPT][DIM], eW[RPT][DIM];
@@ -562,9 +590,9 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     // bank-aware order, ensure_sorted_tree); the first round is predicated below p0, the last
     // (partial) one above p1, so their index loads are in flight together
     auto range_sum = [&](int p0, int p1) -> double {
-        double acc[kSortIlp];
+        double acc[ILP];
 #pragma unroll
-        for (int u = 0; u < kSortIlp; ++u) acc[u] = 0.0;
+        for (int u = 0; u < ILP; ++u) acc[u] = 0.0;
         int p = (p0 & ~63) + tid;
         if (fast && p0 < p1) {
 #if CVQ_SORT_PREFETCH
@@ -573,82 +601,82 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
             // Loads run up to a round past p1 (the lists carry kSortIdxPad zero words) and from
             // p0 rounded down to 64 (>= 0): unconditional, the first and last rounds select their
             // out-of-range nodes away
-            uint32_t cn[kSortIlp];
+            uint32_t cn[ILP];
             const uint32_t* ip = G.idx + p;                // this thread's words of the next round
             {                                              // first round: positions below p0 masked
-                uint32_t c[kSortIlp];
+                uint32_t c[ILP];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) c[u] = ip[u * NT];
-                ip += kSortIlp * NT;
+                for (int u = 0; u < ILP; ++u) c[u] = ip[u * NT];
+                ip += ILP * NT;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) cn[u] = ip[u * NT];
+                for (int u = 0; u < ILP; ++u) cn[u] = ip[u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) {
+                for (int u = 0; u < ILP; ++u) {
                     const int q = p + u * NT;
                     const double v = node_fast(c[u]);
                     acc[u] += (q >= p0 && q < p1) ? v : 0.0;
                 }
-                p += kSortIlp * NT;
+                p += ILP * NT;
             }
-            uint32_t cm[kSortIlp];
+            uint32_t cm[ILP];
             // full rounds in pairs, the word buffers alternating (no register copies)
-            for (; p + (2 * kSortIlp - 1) * NT < p1; p += 2 * kSortIlp * NT) {
-                ip += kSortIlp * NT;
+            for (; p + (2 * ILP - 1) * NT < p1; p += 2 * ILP * NT) {
+                ip += ILP * NT;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) cm[u] = ip[u * NT];
+                for (int u = 0; u < ILP; ++u) cm[u] = ip[u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cn[u]);
-                ip += kSortIlp * NT;
+                for (int u = 0; u < ILP; ++u) acc[u] += node_fast(cn[u]);
+                ip += ILP * NT;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) cn[u] = ip[u * NT];
+                for (int u = 0; u < ILP; ++u) cn[u] = ip[u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cm[u]);
+                for (int u = 0; u < ILP; ++u) acc[u] += node_fast(cm[u]);
             }
-            if (p + (kSortIlp - 1) * NT < p1) {            // an odd full round
-                ip += kSortIlp * NT;
+            if (p + (ILP - 1) * NT < p1) {            // an odd full round
+                ip += ILP * NT;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) cm[u] = ip[u * NT];
+                for (int u = 0; u < ILP; ++u) cm[u] = ip[u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(cn[u]);
+                for (int u = 0; u < ILP; ++u) acc[u] += node_fast(cn[u]);
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) cn[u] = cm[u];
-                p += kSortIlp * NT;
+                for (int u = 0; u < ILP; ++u) cn[u] = cm[u];
+                p += ILP * NT;
             }
             if (p < p1) {                                  // last round: positions from p1 on masked
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) {
+                for (int u = 0; u < ILP; ++u) {
                     const double v = node_fast(cn[u]);
                     acc[u] += p + u * NT < p1 ? v : 0.0;
                 }
             }
 #else
             {                                              // first round: positions below p0 masked
-                uint32_t c[kSortIlp];
+                uint32_t c[ILP];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) {
+                for (int u = 0; u < ILP; ++u) {
                     const int q = p + u * NT;
                     c[u] = (q >= p0 && q < p1) ? G.idx[q] : 0u;
                 }
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) {
+                for (int u = 0; u < ILP; ++u) {
                     const int q = p + u * NT;
                     if (q >= p0 && q < p1) acc[u] += node_fast(c[u]);
                 }
-                p += kSortIlp * NT;
+                p += ILP * NT;
             }
-            for (; p + (kSortIlp - 1) * NT < p1; p += kSortIlp * NT) {
-                uint32_t c[kSortIlp];
+            for (; p + (ILP - 1) * NT < p1; p += ILP * NT) {
+                uint32_t c[ILP];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) c[u] = G.idx[p + u * NT];
+                for (int u = 0; u < ILP; ++u) c[u] = G.idx[p + u * NT];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) acc[u] += node_fast(c[u]);
+                for (int u = 0; u < ILP; ++u) acc[u] += node_fast(c[u]);
             }
             if (p < p1) {
-                uint32_t c[kSortIlp];
+                uint32_t c[ILP];
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u) c[u] = p + u * NT < p1 ? G.idx[p + u * NT] : 0u;
+                for (int u = 0; u < ILP; ++u) c[u] = p + u * NT < p1 ? G.idx[p + u * NT] : 0u;
 #pragma unroll
-                for (int u = 0; u < kSortIlp; ++u)
+                for (int u = 0; u < ILP; ++u)
                     if (p + u * NT < p1) acc[u] += node_fast(c[u]);
             }
 #endif
@@ -656,9 +684,9 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
             for (p = p0 + tid; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
         }
 #pragma unroll
-        for (int h = 1; h < kSortIlp; h <<= 1)
+        for (int h = 1; h < ILP; h <<= 1)
 #pragma unroll
-            for (int u = 0; u + h < kSortIlp; u += 2 * h) acc[u] += acc[u + h];
+            for (int u = 0; u + h < ILP; u += 2 * h) acc[u] += acc[u + h];
         return acc[0];
     };
     int parity = 0;
