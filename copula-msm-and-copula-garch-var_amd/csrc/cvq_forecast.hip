@@ -916,6 +916,12 @@ __global__ __launch_bounds__(256) void k_msm_supscan_w(const double* __restrict_
 // collapse onto the asset's unique vols in state order (Q14) into fbs.  Every vector normalised
 // after each factor / step (positive factors cancel).
 constexpr int kWinGroup = 16;                                    // windows per workgroup = kScanB
+#ifndef CVQ_SCAN_STEP_NORM
+#define CVQ_SCAN_STEP_NORM 4       // partial-block filter steps between normalisations (1: every step)
+#endif
+#ifndef CVQ_SCANWIN_ABL
+#define CVQ_SCANWIN_ABL 0          // ablation builds only (wrong tables): 1 skips the partial-block steps, 2 the factors
+#endif
 template <int K>
 __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const double* __restrict__ r, long long N,
                                                        const double* __restrict__ Gf, long long gstride,
@@ -946,7 +952,11 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
     double x[WPW];
     auto wsum = [&](double v) { return wave_total(act ? v : 0.0); };   // over the wave's S state lanes
     // filter steps i in [i0, i1) (i1 - i0 <= 64) for window m when i lies in its range [a_m, b_m);
-    // the returns r[i0 ..] are loaded once, one per lane, and broadcast by readlane
+    // the returns r[i0 ..] are loaded once, one per lane, and broadcast by readlane.  A vector is
+    // normalised every kStepNorm steps and at its range's last step (positive scale factors cancel,
+    // as between the block products; four unnormalised steps stay far inside the double range), so
+    // three of four steps skip the wave-wide sum that otherwise closes every step's chain
+    constexpr int kStepNorm = CVQ_SCAN_STEP_NORM;
     auto steps = [&](long long i0, long long i1, const long long (&a)[WPW], const long long (&b)[WPW]) {
         const double rl = (i0 + lane < i1) ? r[i0 + lane] : 0.0;
 #pragma unroll 1
@@ -971,8 +981,11 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
                 bfly(std::integral_constant<int, 4>{});
                 if constexpr (K == 6) bfly(std::integral_constant<int, 5>{});
                 v *= ci;
-                const double tot = wsum(v);
-                if (on) x[m] = v * (1.0 / tot);
+                if ((li % kStepNorm) == kStepNorm - 1 || i == b[m] - 1) {   // wave-uniform
+                    const double tot = wsum(v);
+                    v = v * (1.0 / tot);
+                }
+                if (on) x[m] = v;
             }
         }
     };
@@ -986,7 +999,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
             a[m] = tw[m];
             b[m] = bend;
         }
-        steps(a[0], bend, a, b);                                 // this wave's first window starts at a[0]
+        if (CVQ_SCANWIN_ABL != 1) steps(a[0], bend, a, b);       // this wave's first window starts at a[0]
     }
     // 2. full blocks lo_b .. H (shared), then G_{H+1} for the windows with hi_b = H + 1
     const long long lo_b = b0 + 1, H = (t0 + n_in - 1) / kScanB - 1;
@@ -1018,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
 #pragma unroll
     for (int m = 0; m < WPW; ++m) extra |= live[m] && hib[m] == H + 1;
     extra = __syncthreads_or(extra);
-    const long long nf = cnt + (extra ? 1 : 0);
+    const long long nf = CVQ_SCANWIN_ABL == 2 ? 0 : cnt + (extra ? 1 : 0);
     constexpr int FE = S * S / 256;                              // factor entries per thread
     double fn[FE];                                               // the next factor, loaded a factor ahead
     if (nf > 0) {
@@ -1068,7 +1081,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
             lo = min(lo, a[m]);
             hi = max(hi, b[m]);
         }
-        if (hi > lo) steps(lo, hi, a, b);
+        if (hi > lo && CVQ_SCANWIN_ABL != 1) steps(lo, hi, a, b);
     }
     // 4. collapse onto unique vols, states in order (Q14): lane u < q of the wave sums its
     // windows' states mapped to u (the vectors through LDS; the last barrier freed xs)

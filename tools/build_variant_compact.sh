@@ -26,4 +26,4 @@ for s in st_msm_8 st_msm_0 st_gar_8 st_gar_0 ga_msm ga_gar pl_msm pl_gar; do
 done
 for p in $pids; do wait $p; done        # set -e: a failed slice stops the script
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libcvq.so build/cvq_plan.o build/cvq_forecast.o \
-    $out/cvq_compact.o build/cvq_sorted.o $objs
+    $out/cvq_compact.o build/cvq_sorted.o build/cvq_si_*.o $objs
