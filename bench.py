@@ -31,7 +31,10 @@ Prints ONE JSON line (rank 0).
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL).  Default weak scaling
+Multi-GPU: one process per GPU (torch.distributed, RCCL).  `python bench.py --gpus N` with no
+launcher around it starts its N ranks itself (torch.distributed.run as a child process, before
+anything touches the GPU, exiting with its return code); under a launcher WORLD_SIZE must equal
+--gpus.  Default weak scaling
 (--dates-per-gpu, default the config's T, per rank); --global-dates G solves G dates
 split into contiguous blocks of ceil(G / N) (BASELINE configs 3/4/5: 5000 / 2000 / 5000
 "sharded over 8"), strong scaling.  Both run every rank's block through
@@ -109,6 +112,30 @@ def build_inputs(cfg, T_total, rank, world, device):
         ipt, uvs, ggp = tables.sigma_integration_params(block, c.n_in, c.model, c.model_params(), c.num_points, device)
     t_fc = time.time() - t0
     return c, ipt, uvs, ggp, ptf_mean, per, t_fc, block
+
+
+def launch_ranks(a, argv):
+    """`--gpus N` (N > 1) without a launcher: run this same command under torch.distributed.run
+    with N ranks on this node (rendezvous on 127.0.0.1) as a child process and return its exit
+    code.  Called before torch is imported, so this process never initialises the GPU.
+    Under a launcher (WORLD_SIZE set) the world size must equal --gpus."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != a.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={env_world} (launcher) but --gpus {a.gpus}: "
+                             "they must agree (n_gpus would misreport the run)")
+        return None
+    if a.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, cwd=REPO).returncode
 
 
 def main():
@@ -474,4 +501,7 @@ def _cpu_model():
 
 
 if __name__ == "__main__":
+    _rc = launch_ranks(parse(), sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
     main()

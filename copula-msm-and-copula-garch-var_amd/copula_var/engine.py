@@ -194,11 +194,16 @@ class QuadraturePlan:
             self._wide.enable_timing(self._timing)
 
     def kernel_time(self, kind: str) -> Tuple[float, int]:
-        """(total milliseconds, launches) of one kernel kind since enable_timing()."""
+        """(total milliseconds, launches) of one kernel kind since enable_timing(), summed over
+        this plan and its auto-routed sibling (solves above v_cap run there)."""
         ms, n = C.c_double(), C.c_int32()
         N.check(N.lib().cvq_plan_kernel_time(self._h, self.KERNELS[kind], C.byref(ms), C.byref(n)),
                 "cvq_plan_kernel_time")
-        return float(ms.value), int(n.value)
+        tot, cnt = float(ms.value), int(n.value)
+        if self._wide is not None:
+            wm, wn = self._wide.kernel_time(kind)
+            tot, cnt = tot + wm, cnt + wn
+        return tot, cnt
 
     def count_nodes(self, on: bool = True) -> None:
         """Record, in the following solves, how many quadrature nodes each date evaluates
@@ -209,7 +214,10 @@ class QuadraturePlan:
             self._wide.count_nodes(on)
 
     def nodes_evaluated(self) -> int:
-        """Nodes evaluated by the last counted solve, summed over its dates."""
+        """Nodes evaluated by the last counted solve, summed over its dates (read from the
+        sibling plan when the auto rule routed that solve there)."""
+        if self._last is not None and self._last is not self:
+            return self._last.nodes_evaluated()
         n = C.c_int64()
         N.check(N.lib().cvq_plan_nodes_evaluated(self._h, C.byref(n)), "cvq_plan_nodes_evaluated")
         return int(n.value)
@@ -270,6 +278,7 @@ class QuadraturePlan:
         """Drop-in for calc_var (calc_var_class.py:95-177): returns (VaR (T,), iterations)."""
         args = solve_args(ptf_mean, obj_var, first_guess, second_guess, **consts)
         target = self._route(self._top(args))
+        self._last = target
         if target is not self:
             return target.calc_var(ptf_mean, obj_var, first_guess, second_guess, **consts)
         out = np.empty(self.T)

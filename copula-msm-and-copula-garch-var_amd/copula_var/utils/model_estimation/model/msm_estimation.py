@@ -43,12 +43,12 @@ class MSMEstimation(VaRCalculationMethod):
             results[ticker] = SharedCacheCopulaMSMVaR.cache[key]
         return results
 
-    @staticmethod
-    def calculate_marginals_and_densities_in_sample(in_sample_dict, in_sample_params, k):
+    def calculate_marginals_and_densities_in_sample(self, in_sample_dict, in_sample_params, k):
         """msm_estimation.py:55-120: per ticker (cached under (ticker, 'marginals_k'))
         the filtered-probability-weighted normal cdf / pdf of the in-sample returns
-        (calc_marginals.py:7-30; one device filter pass, cvq_msm_marginals), stacked
-        (N-1, dim), and the 2**k vol states."""
+        (calc_marginals.py:7-30; one device filter pass, cvq_msm_marginals, on this
+        adapter's device -- set_device), stacked (N-1, dim), and the 2**k vol states.
+        (The reference's is a staticmethod; here it reads the instance's device.)"""
         marg, dens, vs = [], [], []
         for ticker, params in in_sample_params.items():
             key = (ticker, f"marginals_{k}")
@@ -56,7 +56,7 @@ class MSMEstimation(VaRCalculationMethod):
                 op = params["optimal_params"]
                 m, d, v = insample.msm_marginals_densities_device(
                     np.asarray(in_sample_dict[ticker], dtype=np.float64), k, op["m_0"], op["sig"], op["b"],
-                    op["gamma"], MSMEstimation.device)
+                    op["gamma"], self.device)
                 SharedCacheCopulaMSMVaR.cache[key] = {"marginals": m, "densities": d, "vol_states": v}
             c = SharedCacheCopulaMSMVaR.cache[key]
             marg.append(np.asarray(c["marginals"]).reshape(-1, 1))

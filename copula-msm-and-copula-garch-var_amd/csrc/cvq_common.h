@@ -101,3 +101,29 @@ int make_tconst(double nu, TConst* tk, double** d_cf);
     do {                                                                           \
         if (!(cond)) { cvq::set_error(msg); return (code); }                        \
     } while (0)
+
+namespace cvq {
+// The calling thread's current HIP device, restored when an entry point returns: the library
+// switches to its plan's / argument's device for its own calls, and must not leave the caller
+// (torch shares the process's current device) on another GPU.
+struct DeviceScope {
+    int prev = -1;
+    DeviceScope() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+}
+
+// switch to device `dev` until the enclosing scope ends (range-checked; one per scope)
+#define CVQ_DEVICE_SCOPE(dev)                                                      \
+    cvq::DeviceScope _cvq_device_scope;                                            \
+    do {                                                                           \
+        int _nd = 0;                                                               \
+        CVQ_HIP_CHECK(hipGetDeviceCount(&_nd));                                    \
+        CVQ_REQUIRE((dev) >= 0 && (dev) < _nd, CVQ_ERR_INVALID, "device index out of range"); \
+        CVQ_HIP_CHECK(hipSetDevice(dev));                                          \
+    } while (0)

@@ -18,10 +18,6 @@ int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G
                 "libcvq objects built from different headers (rebuild all)");
     const CompactLaunch L{S, P, G, T, stream, a, tA, tB, pi, st, snaps, hdr, defer, fused, generic};
     const bool msm = S.model == CVQ_MSM;
-#ifdef CVQ_DEV_CFG2                // experiment builds: cfg 2's slice only
-    CVQ_REQUIRE(S.copula == CVQ_STUDENT && msm && S.node_m == 8, CVQ_ERR_UNSUPPORTED, "dev build: cfg 2 only");
-    compact_slice_st_msm_8(L);
-#else
     switch (S.copula) {
         case CVQ_STUDENT:
             if (S.node_m == 8) msm ? compact_slice_st_msm_8(L) : compact_slice_st_gar_8(L);
@@ -30,7 +26,6 @@ int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G
         case CVQ_GAUSSIAN: msm ? compact_slice_ga_msm(L) : compact_slice_ga_gar(L); break;
         default: msm ? compact_slice_pl_msm(L) : compact_slice_pl_gar(L); break;
     }
-#endif
     CVQ_HIP_CHECK(hipGetLastError());
     return CVQ_OK;
 }

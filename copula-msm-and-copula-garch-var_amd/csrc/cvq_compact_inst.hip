@@ -9,8 +9,6 @@ namespace cvq {
 // Student node power: PM = 8 is nu = 6 (b^-4, one rcp per node), PM = 0 the general pow
 #if defined(CVQ_INST_st_msm_8)
 void compact_slice_st_msm_8(const CompactLaunch& L) { launch_pm<CVQ_STUDENT, true, 8>(L); }
-#elif defined(CVQ_DEV_CFG2)
-// experiment builds (tools/build_variant_compact.sh): cfg 2's slice only
 #elif defined(CVQ_INST_st_msm_0)
 void compact_slice_st_msm_0(const CompactLaunch& L) { launch_pm<CVQ_STUDENT, true, 0>(L); }
 #elif defined(CVQ_INST_st_gar_8)

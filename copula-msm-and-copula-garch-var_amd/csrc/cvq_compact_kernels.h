@@ -100,15 +100,6 @@ constexpr int kTlColShift = 11;
 constexpr uint32_t kTlGroupEnd = 1u << 31;
 constexpr int kNoPos = 0x7FFFFFFF;                  // "no such position" in the crossing search
 
-#ifndef CVQ_COMPACT_PRIO
-#define CVQ_COMPACT_PRIO 0
-#endif
-
-template <int P>
-__device__ __forceinline__ void phase_prio() {
-    if constexpr (CVQ_COMPACT_PRIO != 0) __builtin_amdgcn_s_setprio(P);
-}
-
 // Date-independent device tables of a COMPACT plan.
 struct CompactGeom {
     const int16_t* cutfix;    // [n][kCutFixed] cut columns of the fixed levels (per solve arguments)
@@ -392,9 +383,6 @@ __device__ __forceinline__ double generic_node(const StaticDev& S, const double*
     return node_value<COP, MSM, 2>(S, ctx, zc, cg[0], W);
 }
 
-#ifndef CVQ_TABLE_BRANCHY
-#define CVQ_TABLE_BRANCHY 0
-#endif
 // table_entry of grid index i on axis 0 (row) and axis 1 (column) at once: the
 // same arithmetic, with the Student quantile free of data-dependent branches so
 // the two entries' table gathers are in flight together.
@@ -410,12 +398,12 @@ __device__ __forceinline__ void table_pair(const StaticDev& S, const double* __r
             A[ax] = tA[(t * 2 + ax) * S.n + i];
             B[ax] = tB[(t * 2 + ax) * S.n + i];
         }
-    } else if constexpr (COP == CVQ_STUDENT && !CVQ_TABLE_BRANCHY) {
+    } else if constexpr (COP == CVQ_STUDENT) {
         double u[2], pdf[2];
 #pragma unroll
         for (int ax = 0; ax < 2; ++ax) marginal_u<MSM>(S, a, t * 2 + ax, ax, i, &u[ax], &pdf[ax]);
         double z[2];
-        if constexpr (NUI > 0 && CVQ_TABLE_INT_NU) {
+        if constexpr (NUI > 0) {
 #pragma unroll
             for (int ax = 0; ax < 2; ++ax) z[ax] = stdtrit_tab_int<NUI>(S.tk, u[ax]);   // student.py:102
 #pragma unroll
@@ -533,10 +521,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     };
     // nodes this thread evaluated (stamps only: added to stamps[28] per date, zeroed by the host)
     int nev = 0;
-    // issue priority by phase (CVQ_COMPACT_PRIO): the SIMD arbiter favours older waves, so the
-    // last date to arrive on a CU lags the others through every phase; a wave that is further
-    // along lowers its priority so the dates sharing a CU keep pace with each other
-    phase_prio<3>();
     stamp(0);
     if (stamps && tid == 0) {
         stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
@@ -587,12 +571,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (!own[k]) continue;
         const int i = row[k];
         double A[2], B[2];
-#ifdef CVQ_ABL_TABLES
-        A[0] = A[1] = xv[k] * 0.5;                                  // ablation: z = x / 2 (finite)
-        B[0] = B[1] = 1.0;
-#else
         table_pair<COP, MSM, FUSED, (COP == CVQ_STUDENT && PM == 8) ? 6 : 0>(S, a, tA, tB, t, i, A, B);
-#endif
         double wr, wc;                                             // row / column weight factors
         if constexpr (MSM) {
             wr = wc = 0.0;
@@ -654,7 +633,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // non-finite table entry, whose pi is rank 1 by construction)
     const bool flag = __syncthreads_or(MSM ? (bad & 2) : (bad & 1)) != 0;
     stamp(1);
-    phase_prio<2>();
     const bool rank1 = !(MSM && flag);
     const bool fast = rank1 && (MSM || !flag);
     if constexpr (!GEN) {
@@ -787,7 +765,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         kHi[k] = (own[k] && lo == lo) ? max((int)fixcut(k, hi), kLo[k]) : 0;
     }
     stamp(4);
-    phase_prio<1>();
 
     // ---- (iv) bisection (:250-309); Q2 / Q4 are resolved across dates by the finalize
     double prev = F, prevU = prevU0;
@@ -834,12 +811,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
-#ifdef CVQ_ABL_CNT
-            kM[k] = own[k] ? (kLo[k] + kHi[k]) >> 1 : 0;
-#else
             kM[k] = !own[k] ? 0 : (tcut && hc < kcn) ? kmt[k]
                   : grid_count(sx, bk, G, inner_coord(S, mid, lev[k]), kLo[k], kHi[k]);   // Q10
-#endif
             ka[k] = ustack ? kLo[k] : kM[k];
             kb[k] = ustack ? kM[k] : kHi[k];
         }
@@ -895,7 +868,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // so each remaining level's decision "F(mid) < obj" is "mid < v_c" with v_c the first
     // tie-group end where !(F < obj), and its nonzero bit is "mid >= v_z", v_z the first
     // where F != 0 -- one lane then walks the remaining levels without sums.
-    phase_prio<0>();
     if (tabc && it < P.K) {
         constexpr int NPT = kBlkPerThread;
         const int cnt = max(nbr_next, 0);
@@ -1008,11 +980,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         }
         __syncthreads();
         stamp(29);
-#ifdef CVQ_ABL_TAIL
-        if (false) {
-#else
         if ((tid >> 6) == (leader >> 6)) {
-#endif
             // this lane's entries lane + 64 m: (v*, value); padding v* = NaN is in no interval
             const int tot = min(total, kTailCap);
             double tx[kTailPerLane], ty[kTailPerLane];

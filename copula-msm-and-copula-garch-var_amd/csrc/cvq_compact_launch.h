@@ -39,9 +39,7 @@ constexpr long long kGenericGrid = 512;
 template <int COP, bool MSM, int PM, bool FUSED, int RPT>
 void launch_r(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
-    // experiment knob: extra dynamic LDS per workgroup (caps resident dates per CU)
-    static const size_t lds_pad = getenv("CVQ_COMPACT_LDS_PAD") ? (size_t)atol(getenv("CVQ_COMPACT_LDS_PAD")) : 0;
-    const size_t lds_fast = compact_lds_bytes<COP, false>(L.S.n, NT, L.G.nb) + lds_pad;
+    const size_t lds_fast = compact_lds_bytes<COP, false>(L.S.n, NT, L.G.nb);
     const size_t lds_gen = compact_lds_bytes<COP, true>(L.S.n, NT, L.G.nb);
     hipLaunchKernelGGL((k_compact<COP, MSM, NT, RPT, PM, FUSED, false>), dim3((unsigned)L.T), dim3(NT), lds_fast, L.stream,
                        L.S, L.P, L.G, L.a, L.tA, L.tB, L.pi, L.st, L.snaps, L.hdr, L.generic ? L.defer : nullptr, L.T);
@@ -55,23 +53,14 @@ template <int COP, bool MSM, int PM, bool FUSED>
 void launch_f(const CompactLaunch& L) {
     constexpr int NT = CVQ_COMPACT_NT;
     const int rpt = (L.S.n + NT - 1) / NT;
-#ifdef CVQ_DEV_CFG2            // experiment builds (tools/build_variant_compact.sh): cfg 2's instance only
-    (void)rpt;
-    launch_r<COP, MSM, PM, FUSED, 1>(L);
-#else
     if (rpt <= 1) launch_r<COP, MSM, PM, FUSED, 1>(L);
     else launch_r<COP, MSM, PM, FUSED, 2>(L);
-#endif
 }
 
 template <int COP, bool MSM, int PM>
 void launch_pm(const CompactLaunch& L) {
-#ifdef CVQ_DEV_CFG2
-    launch_f<COP, MSM, PM, true>(L);
-#else
     if (L.fused) launch_f<COP, MSM, PM, true>(L);
     else launch_f<COP, MSM, PM, false>(L);
-#endif
 }
 
 // the instance slices (cvq_compact_inst.hip, one object per CVQ_INST_* in the Makefile)

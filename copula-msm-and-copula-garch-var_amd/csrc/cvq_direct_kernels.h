@@ -42,7 +42,6 @@ __device__ __forceinline__ double pow_node_t(double b, int m, double ex) {
 }
 
 // mode 0: calc_var solve (snapshots + header);  mode 1: one slab per date (compute_integral);
-// mode 2: table staging + row setup only (profiling ablation).
 //
 // Thread `slot` of the 256-thread block owns rows slot + 256 k (k < RPT) for the
 // whole solve.  Row constants (outer table values, row weights G) live in
@@ -65,13 +64,7 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int NT = 256;
     const long long t = blockIdx.x;
-#if CVQ_DIRECT_ROT
-    // wave w owns row block (w + t) mod 4: the long rows of triangular slabs land on a
-    // different SIMD for each of the dates sharing a CU
-    const int n = S.n, tid = threadIdx.x, slot = ((((tid >> 6) + (int)t) & 3) << 6) | (tid & 63);
-#else
     const int n = S.n, tid = threadIdx.x, slot = tid;
-#endif
     // Column records, one per inner index j, CS doubles each (16-B aligned):
     //   [0] z_j, [1..QT] F'_b[j], then B_j for the non-folded paths.
     // A lane's operands for a node are CS contiguous doubles (ds_read_b128 x CS/2);
@@ -148,10 +141,6 @@ __global__ __launch_bounds__(256, 4) void k_direct(StaticDev S, SolveConst P, co
     }
     __syncthreads();
     stamp(1);
-    if (mode == 2) {
-        if (tid == 0) snaps[t * P.stride] = ctx[0].z0 + G[0][0] + col[(n - 1) * CS];
-        return;
-    }
     auto cnt = [&](int k, double v, int klo, int khi) {
         const double g = inner_coord(S, v, lev[k]);   // var_function (Q10), exact FP64
         return count_le(sx, g, klo, khi);

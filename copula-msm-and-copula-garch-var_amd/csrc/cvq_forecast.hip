@@ -919,9 +919,6 @@ constexpr int kWinGroup = 16;                                    // windows per 
 #ifndef CVQ_SCAN_STEP_NORM
 #define CVQ_SCAN_STEP_NORM 4       // partial-block filter steps between normalisations (1: every step)
 #endif
-#ifndef CVQ_SCANWIN_ABL
-#define CVQ_SCANWIN_ABL 0          // ablation builds only (wrong tables): 1 skips the partial-block steps, 2 the factors
-#endif
 template <int K>
 __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const double* __restrict__ r, long long N,
                                                        const double* __restrict__ Gf, long long gstride,
@@ -999,7 +996,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
             a[m] = tw[m];
             b[m] = bend;
         }
-        if (CVQ_SCANWIN_ABL != 1) steps(a[0], bend, a, b);       // this wave's first window starts at a[0]
+        steps(a[0], bend, a, b);       // this wave's first window starts at a[0]
     }
     // 2. full blocks lo_b .. H (shared), then G_{H+1} for the windows with hi_b = H + 1
     const long long lo_b = b0 + 1, H = (t0 + n_in - 1) / kScanB - 1;
@@ -1031,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
 #pragma unroll
     for (int m = 0; m < WPW; ++m) extra |= live[m] && hib[m] == H + 1;
     extra = __syncthreads_or(extra);
-    const long long nf = CVQ_SCANWIN_ABL == 2 ? 0 : cnt + (extra ? 1 : 0);
+    const long long nf = cnt + (extra ? 1 : 0);
     constexpr int FE = S * S / 256;                              // factor entries per thread
     double fn[FE];                                               // the next factor, loaded a factor ahead
     if (nf > 0) {
@@ -1081,7 +1078,7 @@ __global__ __launch_bounds__(256) void k_msm_scanwin_w(MsmParamsN PN, const doub
             lo = min(lo, a[m]);
             hi = max(hi, b[m]);
         }
-        if (hi > lo && CVQ_SCANWIN_ABL != 1) steps(lo, hi, a, b);
+        if (hi > lo) steps(lo, hi, a, b);
     }
     // 4. collapse onto unique vols, states in order (Q14): lane u < q of the wave sums its
     // windows' states mapped to u (the vectors through LDS; the last barrier freed xs)
@@ -1662,9 +1659,7 @@ int launch_blocked_k(int k, const MsmParamsN& P, int dim, const double* cond, lo
 // (one wavefront per superblock scan); k = 5, 6 the wide variant (no stored prefixes, 256-thread
 // superblock scans, one wavefront per window); windows longer than two blocks.
 bool msm_scan_ok(int k, long long n_in) {
-    static const bool on = !getenv("CVQ_MSM_SCAN") || atoi(getenv("CVQ_MSM_SCAN")) != 0;   // A/B switch
-    static const bool wide = !getenv("CVQ_MSM_SCAN_WIDE") || atoi(getenv("CVQ_MSM_SCAN_WIDE")) != 0;
-    return on && k >= 2 && (k <= 4 || (wide && k <= 6)) && n_in > 2 * kScanB;
+    return k >= 2 && k <= 6 && n_in > 2 * kScanB;
 }
 
 struct ScanLayout {                 // doubles of each scan buffer, per asset
@@ -1748,13 +1743,6 @@ void launch_msm_ll(const MsmParams* P, long long B, const double* r, long long N
     hipLaunchKernelGGL(k_msm_loglik<K>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, P, B, r, N, out);
 }
 
-int check_device(int device) {
-    int n = 0;
-    CVQ_HIP_CHECK(hipGetDeviceCount(&n));
-    CVQ_REQUIRE(device >= 0 && device < n, CVQ_ERR_INVALID, "device index out of range");
-    CVQ_HIP_CHECK(hipSetDevice(device));
-    return CVQ_OK;
-}
 
 }  // namespace
 
@@ -1796,8 +1784,8 @@ int32_t cvq_msm_tables(int32_t device, void* stream, int32_t dim, int32_t k, con
             M.u[d][s2] = (uint8_t)state_map[d * S + s2];
         }
     }
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     hipStream_t st = (hipStream_t)stream;
     const long long N = n_in + T - 1;
     const bool scan = msm_scan_ok(k, n_in);
@@ -1902,8 +1890,7 @@ int32_t cvq_sigma_tables(int32_t device, void* stream, int32_t model, int32_t di
             pp += 3;
         }
     }
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
     hipStream_t st = (hipStream_t)stream;
     const long long N = n_in + T - 1;
     CVQ_HIP_CHECK(hipMemsetAsync(d_err, 0, sizeof(int32_t), st));
@@ -1939,8 +1926,8 @@ int32_t cvq_msm_filter(int32_t device, int32_t k, double m0, double sigma, doubl
     CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
     CVQ_REQUIRE(n_in >= 1 && T >= 1, CVQ_ERR_INVALID, "n_in and T must be >= 1");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     MsmParamsN P{};
     P.a[0] = msm_params(k, m0, sigma, b, gamma);
     const int S = 1 << k;
@@ -1968,8 +1955,8 @@ int32_t cvq_msm_marginals(int32_t device, int32_t k, double m0, double sigma, do
     CVQ_REQUIRE(returns && marg_out && dens_out, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
     CVQ_REQUIRE(N >= 2, CVQ_ERR_INVALID, "N must be >= 2 (the marginals pair step i with return i - 1)");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     const MsmParams P = msm_params(k, m0, sigma, b, gamma);
     DevBuf rin, dm, dd;
     DevInt err;
@@ -2004,8 +1991,8 @@ int32_t cvq_garch_forecast(int32_t device, double omega, double alpha, double be
     CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(omega > 0 && alpha > 0 && beta > 0 && alpha + beta < 1, CVQ_ERR_INVALID,
                 "GARCH parameters must be positive with alpha + beta < 1 (garch/estimation.py:22-38)");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf rin, dout;
     const double* d_r;
     double* d_out;
@@ -2027,8 +2014,8 @@ int32_t cvq_garch_forecast_pq(int32_t device, int32_t p, int32_t q, const double
     for (int i = 1; i <= p + q; ++i) { pos = pos && params[i] > 0; s += params[i]; }
     CVQ_REQUIRE(pos && s < 1, CVQ_ERR_INVALID,
                 "GARCH parameters must be positive with sum(alpha) + sum(beta) < 1 (garch/estimation.py:22-38)");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf pin, rin, dout;
     const double *d_p, *d_r;
     double* d_out;
@@ -2048,8 +2035,8 @@ int32_t cvq_garch_forecast_pq(int32_t device, int32_t p, int32_t q, const double
 int32_t cvq_ukf_forecast(int32_t device, double a, double l, double q, const double* returns_c, int64_t n_in,
                          int64_t T, double* out, int32_t mem) {
     CVQ_REQUIRE(returns_c && out, CVQ_ERR_INVALID, "NULL argument");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf rin, dout;
     DevInt err;
     const double* d_r;
@@ -2071,8 +2058,8 @@ int32_t cvq_msm_loglik(int32_t device, int32_t k, const double* params, int64_t 
                        double* out, int32_t mem) {
     CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
     CVQ_REQUIRE(k >= 1 && k <= 7, CVQ_ERR_UNSUPPORTED, "MSM k must be in [1, 7]");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     std::vector<double> hp((size_t)B * 4);
     if (mem == CVQ_MEM_DEVICE) CVQ_HIP_CHECK(hipMemcpy(hp.data(), params, hp.size() * sizeof(double), hipMemcpyDeviceToHost));
     else std::copy(params, params + hp.size(), hp.begin());
@@ -2109,8 +2096,8 @@ int32_t cvq_msm_loglik(int32_t device, int32_t k, const double* params, int64_t 
 int32_t cvq_garch_loglik(int32_t device, const double* params, int64_t B, const double* returns, int64_t N,
                          double* out, int32_t mem) {
     CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf pin, rin, dout;
     const double *d_p, *d_r;
     double* d_out;
@@ -2126,8 +2113,8 @@ int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* 
     CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
     CVQ_REQUIRE(p >= 1 && q >= 1 && p <= kGarchMaxPQ && q <= kGarchMaxPQ, CVQ_ERR_UNSUPPORTED,
                 "GARCH orders must be 1 <= p, q <= 4");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf pin, rin, dout;
     const double *d_p, *d_r;
     double* d_out;
@@ -2147,8 +2134,8 @@ int32_t cvq_garch_loglik_pq(int32_t device, int32_t p, int32_t q, const double* 
 int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B, const double* returns, int64_t N, double* out,
                        int32_t mem) {
     CVQ_REQUIRE(params && returns && out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     DevBuf pin, rin, dout;
     const double *d_p, *d_r;
     double* d_out;
@@ -2163,8 +2150,8 @@ int32_t cvq_ukf_loglik(int32_t device, const double* params, int64_t B, const do
 int32_t cvq_ukf_filter(int32_t device, const double* params, int64_t B, const double* returns, int32_t per_candidate,
                        int64_t N, double* ll_out, double* states_out, int32_t mem) {
     CVQ_REQUIRE(params && returns && ll_out && states_out && B >= 1 && N >= 1, CVQ_ERR_INVALID, "bad argument");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     const long long r_stride = per_candidate ? N : 0;
     DevBuf pin, rin, dll, dst;
     const double *d_p, *d_r;
@@ -2186,8 +2173,8 @@ int32_t cvq_special(int32_t device, int32_t fn, double nu, const double* x, int6
     CVQ_REQUIRE(fn >= 0 && fn <= 3, CVQ_ERR_INVALID,
                 "fn must be 0 (t.ppf), 1 (norm.ppf), 2 (erf) or 3 (t.ppf, the solve kernels' nu = 6 path)");
     CVQ_REQUIRE(fn != 3 || nu == 6.0, CVQ_ERR_INVALID, "fn 3 is the integer path for nu = 6");
-    int rc = check_device(device);
-    if (rc) return rc;
+    CVQ_DEVICE_SCOPE(device);
+    int rc = CVQ_OK;
     TConst tk{};
     DevBuf cf;
     if (fn == 0 || fn == 3) {

@@ -538,70 +538,6 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
             pvs[q] = vs[ord[q - c0].second];
         }
     }
-    // Bank-aware order (SORTED, 2-D): the solve's range sums read position q in lane q mod 64
-    // (k_sorted aligns every range to 64), so inside each freely ordered segment the host picks,
-    // position by position, the node whose two 16-B LDS records add the fewest bank-slot
-    // conflicts to its ds_read_b128 lane group (MI355X_MICROARCH.md §LDS) among the next 64 of
-    // the row-major order (tools/lds_sim.py: 9-12 LDS cycles per record read -> see DESIGN.md).
-    static const bool bank_order = !getenv("CVQ_SORT_BANK") || atoi(getenv("CVQ_SORT_BANK")) != 0;   // A/B
-    if (bank_order && p->strategy == CVQ_STRATEGY_SORTED && lay == kLay2) {
-        auto group_of = [](int l) {                            // ds_read_b128 lane groups
-            const int h = l >> 5, m = l & 31;
-            const int g = (m < 4 || (m >= 12 && m < 16) || (m >= 20 && m < 28)) ? 0 : 1;
-            return 2 * h + g;
-        };
-        std::vector<uint32_t> nidx(pidx.begin(), pidx.begin() + G);
-        std::vector<double> nvs(pvs.begin(), pvs.begin() + G);
-        // per segment: a window of the next <= 64 candidates (row-major stream position `next`)
-        struct Seg { int c0, c1, next; bool keep; std::vector<int> win; };
-        std::vector<Seg> segs;
-        for (size_t k = 0; k + 1 < cuts.size(); ++k) {
-            const int c0 = cuts[k], c1 = std::min(cuts[k + 1], G);
-            if (c1 <= c0) continue;
-            bool searchable = false;
-            for (int b = 0; b < 4; ++b) searchable |= c1 - c0 > tcap && c0 >= bpos[b][0] && c1 <= bpos[b][1];
-            segs.push_back({c0, c1, c0, searchable || c1 - c0 < 2, {}});
-        }
-        size_t si = 0;
-        for (int blk = 0; blk < G; blk += 64) {
-            std::vector<uint32_t> ra[4][16], ca[4][16];        // distinct record addresses per group / slot
-            for (int q = blk; q < std::min(blk + 64, G); ++q) {
-                while (segs[si].c1 <= q) ++si;
-                Seg& sg = segs[si];
-                const int g = group_of(q & 63);
-                uint32_t c;
-                double v;
-                if (sg.keep) {
-                    c = pidx[q];
-                    v = pvs[q];
-                } else {
-                    while ((int)sg.win.size() < 64 && sg.next < sg.c1) sg.win.push_back(sg.next++);
-                    int best = 0, bscore = 1 << 30;
-                    for (int k = 0; k < (int)sg.win.size(); ++k) {
-                        const uint32_t w = pidx[sg.win[k]];
-                        const uint32_t a1 = w & 0xFFFFu, a2 = w >> 16;
-                        const std::vector<uint32_t>& v1 = ra[g][(a1 >> 4) & 15];
-                        const std::vector<uint32_t>& v2 = ca[g][(a2 >> 4) & 15];
-                        const int sc = (std::find(v1.begin(), v1.end(), a1) != v1.end() ? 0 : (int)v1.size()) +
-                                       (std::find(v2.begin(), v2.end(), a2) != v2.end() ? 0 : (int)v2.size());
-                        if (sc < bscore) { bscore = sc; best = k; if (sc == 0) break; }
-                    }
-                    const int src = sg.win[best];
-                    sg.win.erase(sg.win.begin() + best);
-                    c = pidx[src];
-                    v = pvs[src];
-                }
-                nidx[q] = c;
-                nvs[q] = v;
-                std::vector<uint32_t>& v1 = ra[g][((c & 0xFFFFu) >> 4) & 15];
-                std::vector<uint32_t>& v2 = ca[g][((c >> 16) >> 4) & 15];
-                if (std::find(v1.begin(), v1.end(), c & 0xFFFFu) == v1.end()) v1.push_back(c & 0xFFFFu);
-                if (std::find(v2.begin(), v2.end(), c >> 16) == v2.end()) v2.push_back(c >> 16);
-            }
-        }
-        std::copy(nidx.begin(), nidx.end(), pidx.begin());
-        std::copy(nvs.begin(), nvs.end(), pvs.begin());
-    }
     if (p->strategy == CVQ_STRATEGY_SWEEP && (lay == kLay2 || lay == kLay2W)) {
         // SWEEP's lanes read positions a chunk apart, not consecutive ones: inside each segment of
         // the two root passes' ranges, pick for every (round, lane) the node whose two LDS records
@@ -812,8 +748,6 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     build_cell_counts(p->hvc, P, compact_tail_cap(), cc, &p->ccount_depth);
     const double blo[4] = {P.vmin, P.sg0, P.sg1, P.fg};      // k_compact's brackets' lower levels
     for (int b = 0; b < 4; ++b) p->bstart[b] = host_ub(p->hvc, blo[b]);
-    static const bool no_cc = getenv("CVQ_COMPACT_COUNT") && atoi(getenv("CVQ_COMPACT_COUNT")) != 0;   // A/B switch
-    if (no_cc) p->ccount_depth = -1;
     if (p->ccount_depth >= 0) {
         CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));   // the previous table may still be read
         if (int rc = dev_alloc(&p->d_ccount, cc.size())) return rc;
@@ -821,9 +755,8 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     }
     // per-row cuts of every tabulated bisection cell's mid (the levels' cnt_r(mid) without a grid
     // search): [4][2^D][n] int16, heap node h of bracket b at (b << D) + h; bounded to 4 MB
-    static const bool no_kcut = getenv("CVQ_LEVEL_CUTS") && atoi(getenv("CVQ_LEVEL_CUTS")) == 0;   // A/B switch
     const int D = p->ccount_depth;
-    p->kcut_ok = !no_kcut && D >= 1 && ((size_t)4 << D) * n * sizeof(int16_t) <= ((size_t)4 << 20);
+    p->kcut_ok = D >= 1 && ((size_t)4 << D) * n * sizeof(int16_t) <= ((size_t)4 << 20);
     if (p->kcut_ok) {
         std::vector<int16_t> kc(((size_t)4 << D) * n, 0);
         const double br[4][2] = {{P.vmin, P.sg0}, {P.sg0, P.fg}, {P.sg1, P.vmax}, {P.fg, P.sg1}};
@@ -960,15 +893,14 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
-        // profiling only: CVQ_DIRECT_ABLATE=2 (tables-only ablation), CVQ_STAMPS=1 (phase stamps)
-        static const int dbg_mode = getenv("CVQ_DIRECT_ABLATE") ? atoi(getenv("CVQ_DIRECT_ABLATE")) : 0;
+        // profiling only: CVQ_STAMPS=1 (phase stamps)
         static const bool dbg_stamps = getenv("CVQ_STAMPS") != nullptr;
         double* st = nullptr;
         if (dbg_stamps) {
             if (int rc = ensure_stamps(p)) return rc;
             st = (double*)p->d_stamps;
         }
-        return launch_direct(p, P, dbg_mode == 2 ? 2 : 0, nullptr, st, snaps, hdr);
+        return launch_direct(p, P, 0, nullptr, st, snaps, hdr);
     }
     int tpd, rpt;
     CVQ_REQUIRE(pick_solve_shape(p->S.nrows, &tpd, &rpt) == CVQ_OK, CVQ_ERR_UNSUPPORTED,
@@ -1138,8 +1070,7 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.ptf_mean = a.ptf_mean;
     P.fin_var = nullptr;
     P.fin_err = nullptr;
-    static const bool serial_walk = getenv("CVQ_SERIAL_WALK") && atoi(getenv("CVQ_SERIAL_WALK")) != 0;   // A/B
-    P.exact_walk = !serial_walk && dyadic_walk_ok(a, K) ? 1 : 0;
+    P.exact_walk = dyadic_walk_ok(a, K) ? 1 : 0;
     return P;
 }
 
@@ -1205,6 +1136,7 @@ int32_t cvq_device_count(int32_t* count) {
 }
 
 int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(s != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     *out = nullptr;
     CVQ_REQUIRE(s->model >= CVQ_MSM && s->model <= CVQ_UKF, CVQ_ERR_INVALID, "unknown model kind");
@@ -1367,8 +1299,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     if (sorted_family(p)) {                            // reachable nodes sorted by their exact threshold v*
         std::vector<uint32_t> idx;
         // SWEEP + Student with an integer power: 32-B records with the folded scale (kLay2W)
-        static const bool fold = !getenv("CVQ_SWEEP_FOLD") || atoi(getenv("CVQ_SWEEP_FOLD")) != 0;   // A/B switch
-        p->layout = (fold && p->strategy == CVQ_STRATEGY_SWEEP && sorted_fold(S.copula, S.dim, S.node_m))
+        p->layout = (p->strategy == CVQ_STRATEGY_SWEEP && sorted_fold(S.copula, S.dim, S.node_m))
                   ? kLay2W : sorted_layout(S.dim, n);
         build_sorted_nodes(p->hx, S, kmax, p->layout, p->hvs, idx);
         const size_t nv = idx.size();
@@ -1425,6 +1356,7 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
 }
 
 int32_t cvq_plan_destroy(cvq_plan* p) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     if (!p) return CVQ_OK;
     (void)hipSetDevice(p->device);
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
@@ -1464,6 +1396,7 @@ int32_t cvq_plan_timing(cvq_plan* p, int32_t enable) {
 }
 
 int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_t* launches) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && total_ms != nullptr && launches != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(kind >= 0 && kind < TK_COUNT, CVQ_ERR_INVALID, "unknown kernel kind");
     double tot = 0.0;
@@ -1482,6 +1415,7 @@ int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_
 }
 
 int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->d_stamps != nullptr, CVQ_ERR_STATE, "no stamps recorded (set CVQ_STAMPS=1; DIRECT, COMPACT or SORTED strategy)");
     CVQ_REQUIRE(count <= p->capStamps * 32, CVQ_ERR_INVALID, "count exceeds the stamp buffer");
@@ -1491,10 +1425,11 @@ int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
 }
 
 int32_t cvq_plan_debug_nodes(cvq_plan* p, uint32_t* host, int64_t count, int32_t* fix) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->d_pidx != nullptr && p->tree_valid, CVQ_ERR_STATE,
                 "no solve-order node list (a SORTED plan builds it at its first solve)");
-    CVQ_REQUIRE(count <= (int64_t)p->S.G, CVQ_ERR_INVALID, "count exceeds the plan's reachable nodes");
+    CVQ_REQUIRE(count >= 0 && count <= (int64_t)p->S.G, CVQ_ERR_INVALID, "count must be in [0, reachable nodes]");
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     CVQ_HIP_CHECK(hipMemcpy(host, p->d_pidx, count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (fix) for (int e = 0; e < 6; ++e) fix[e] = p->fixpos[e];
@@ -1502,6 +1437,7 @@ int32_t cvq_plan_debug_nodes(cvq_plan* p, uint32_t* host, int64_t count, int32_t
 }
 
 int32_t cvq_plan_debug_cuts(cvq_plan* p, int32_t* host, int64_t cap, int32_t* count) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && count != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->tree_valid, CVQ_ERR_STATE, "no solve-order node list (a SORTED plan builds it at its first solve)");
     *count = (int32_t)p->hcuts.size();
@@ -1520,6 +1456,7 @@ int32_t cvq_plan_count_nodes(cvq_plan* p, int32_t enable) {
 }
 
 int32_t cvq_plan_nodes_evaluated(cvq_plan* p, int64_t* total) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && total != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->nodes_valid && p->d_stamps != nullptr, CVQ_ERR_STATE,
                 "no node counts recorded (cvq_plan_count_nodes(plan, 1), then cvq_solve)");
@@ -1539,6 +1476,7 @@ int32_t cvq_set_fast_hint(cvq_plan* p, int32_t on) {
 }
 
 int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, int32_t mem) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && a != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(T > 0, CVQ_ERR_INVALID, "T must be > 0");
     CVQ_REQUIRE(p->S.model != CVQ_MSM || b != nullptr, CVQ_ERR_INVALID, "MSM needs the forecast combinations");
@@ -1584,6 +1522,7 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
 }
 
 int32_t cvq_slab(cvq_plan* p, const double* bounds, double* out, int32_t mem) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && bounds != nullptr && out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(p->T > 0, CVQ_ERR_STATE, "cvq_set_dates must be called first");
     if (mem != CVQ_MEM_DEVICE && materialised(p)) {
@@ -1612,6 +1551,7 @@ int32_t cvq_snap_stride(const cvq_solve_args* a, int32_t* stride) {
 }
 
 int32_t cvq_solve_local(cvq_plan* p, const cvq_solve_args* a, void* d_header, double* d_snaps) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && d_header != nullptr && d_snaps != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;
@@ -1623,6 +1563,7 @@ int32_t cvq_solve_local(cvq_plan* p, const cvq_solve_args* a, void* d_header, do
 
 int32_t cvq_solve_finalize(cvq_plan* p, const cvq_solve_args* a, const void* d_headers, int32_t n_ranks,
                            const double* d_snaps, int64_t dates_per_rank, int64_t T_total, double* d_var) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && a != nullptr && d_headers && d_snaps && d_var, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(n_ranks >= 1 && T_total <= (int64_t)n_ranks * dates_per_rank, CVQ_ERR_INVALID,
                 "T_total exceeds n_ranks * dates_per_rank");
@@ -1651,6 +1592,7 @@ int32_t cvq_packed_block_len(const cvq_solve_args* a, int64_t dates_per_rank, in
 
 int32_t cvq_solve_finalize_packed(cvq_plan* p, const cvq_solve_args* a, const double* d_blocks, int32_t n_ranks,
                                   int64_t dates_per_rank, int64_t T_total, double* d_var) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && a != nullptr && d_blocks && d_var, CVQ_ERR_INVALID, "NULL argument");
     CVQ_REQUIRE(n_ranks >= 1 && dates_per_rank >= 1 && T_total <= (int64_t)n_ranks * dates_per_rank, CVQ_ERR_INVALID,
                 "T_total exceeds n_ranks * dates_per_rank");
@@ -1670,6 +1612,7 @@ int32_t cvq_solve_finalize_packed(cvq_plan* p, const cvq_solve_args* a, const do
 }
 
 int32_t cvq_solve_status(cvq_plan* p, int32_t* iters_out) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
     CVQ_HIP_CHECK(hipSetDevice(p->device));
     int err[3] = {0, 0, 0};
@@ -1681,6 +1624,7 @@ int32_t cvq_solve_status(cvq_plan* p, int32_t* iters_out) {
 }
 
 int32_t cvq_solve(cvq_plan* p, const cvq_solve_args* a, double* var_out, int32_t* iters_out, int32_t mem) {
+    cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && var_out != nullptr, CVQ_ERR_INVALID, "NULL argument");
     int rc = check_args(p, a);
     if (rc) return rc;

@@ -43,11 +43,6 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 constexpr int kQUnroll = 8;
 
 __device__ __forceinline__ double wave_sum(double v) {
-#ifdef CVQ_SHFL_REDUCE
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-#endif
     v += dpp_f64<0xB1>(v);      // quad_perm [1,0,3,2]
     v += dpp_f64<0x4E>(v);      // quad_perm [2,3,0,1]
     v += dpp_f64<0x141>(v);     // row_half_mirror
@@ -110,9 +105,6 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
     }
 }
 
-#ifndef CVQ_TABLE_INT_NU
-#define CVQ_TABLE_INT_NU 1
-#endif
 // NUI > 0 (with TAB): the Student nu is the integer NUI -- quantile tail variable by root_nu,
 // B = pdf (1 + z^2/nu)^((nu+1)/2) / g_uni without divisions (~1 ulp from the reference's
 // arithmetic; the VaR tolerates ~1e-8 relative node noise)
@@ -121,7 +113,7 @@ __device__ __forceinline__ void table_entry(const StaticDev& S, const double* __
                                             int i, double* A_out, double* B_out) {
     double u, pdf;
     marginal_u<MSM>(S, a, td, d, i, &u, &pdf);
-    if constexpr (COP == CVQ_STUDENT && TAB && NUI > 0 && CVQ_TABLE_INT_NU) {
+    if constexpr (COP == CVQ_STUDENT && TAB && NUI > 0) {
         const double z = stdtrit_tab_int<NUI>(S.tk, u);                              // student.py:102
         const double pw = pow_half_pos_c<NUI + 1>(fma(z * z, S.inv_nu, 1.0));            // :164-172, uni_m = nu + 1
         *A_out = z;

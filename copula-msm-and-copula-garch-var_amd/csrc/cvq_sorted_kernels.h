@@ -49,9 +49,6 @@ constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisec
 #ifndef CVQ_SORT_ILP
 #define CVQ_SORT_ILP 4
 #endif
-#ifndef CVQ_SORT_PREFETCH
-#define CVQ_SORT_PREFETCH 1        // range sums load the next round's node words a round ahead
-#endif
 // zero words after the node lists: a range sum's prefetch reads up to one round (kSortIlp x the
 // widest workgroup) past its range, SWEEP's 16-B loads up to 4 words
 constexpr int kSortIdxPad = CVQ_SORT_ILP * 1024;
@@ -81,9 +78,6 @@ constexpr int kSortNT = 256;                          // threads per k_sorted wo
 #define CVQ_SWEEP_MIN_WAVES 4                         // SWEEP: <= 128 VGPRs (the pass loop holds the solve state)
 #endif
 constexpr int kSweepCap = 256;
-#ifndef CVQ_SWEEP_EDGE
-#define CVQ_SWEEP_EDGE 1
-#endif
 constexpr int kSweepD0Max = 6;
 constexpr int kSweepDMax = 8;
 
@@ -586,8 +580,8 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         return node_value<COP, MSM, DIM>(S, ctx, zi, Bi, W);
     };
     // sum of the nodes at sorted positions [p0, p1), strided over the workgroup: the rounds start
-    // at p0 rounded down to 64, so position q is always read by lane q mod 64 (the plan's
-    // bank-aware order, ensure_sorted_tree); the first round is predicated below p0, the last
+    // at p0 rounded down to 64, so position q is always read by lane q mod 64; the first round
+    // is predicated below p0, the last
     // (partial) one above p1, so their index loads are in flight together
     auto range_sum = [&](int p0, int p1) -> double {
         double acc[ILP];
@@ -595,7 +589,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         for (int u = 0; u < ILP; ++u) acc[u] = 0.0;
         int p = (p0 & ~63) + tid;
         if (fast && p0 < p1) {
-#if CVQ_SORT_PREFETCH
             // the next round's node words are loaded before this round's nodes are evaluated (a
             // few dates per CU leave too few waves to cover the L2 latency of unpipelined loads).
             // Loads run up to a round past p1 (the lists carry kSortIdxPad zero words) and from
@@ -649,37 +642,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                     acc[u] += p + u * NT < p1 ? v : 0.0;
                 }
             }
-#else
-            {                                              // first round: positions below p0 masked
-                uint32_t c[ILP];
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) {
-                    const int q = p + u * NT;
-                    c[u] = (q >= p0 && q < p1) ? G.idx[q] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) {
-                    const int q = p + u * NT;
-                    if (q >= p0 && q < p1) acc[u] += node_fast(c[u]);
-                }
-                p += ILP * NT;
-            }
-            for (; p + (ILP - 1) * NT < p1; p += ILP * NT) {
-                uint32_t c[ILP];
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) c[u] = G.idx[p + u * NT];
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) acc[u] += node_fast(c[u]);
-            }
-            if (p < p1) {
-                uint32_t c[ILP];
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) c[u] = p + u * NT < p1 ? G.idx[p + u * NT] : 0u;
-#pragma unroll
-                for (int u = 0; u < ILP; ++u)
-                    if (p + u * NT < p1) acc[u] += node_fast(c[u]);
-            }
-#endif
         } else {
             for (p = p0 + tid; p < p1; p += NT) acc[0] += node_generic(G.idx[p]);
         }

@@ -435,9 +435,6 @@ __device__ __forceinline__ double log_node(double b) {
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
-#ifndef CVQ_POW_LIB
-#define CVQ_POW_LIB 0
-#endif
 __device__ __forceinline__ double pow_gen(double b, double ex);
 // b^ex for b >= 1 with ex = -m/2 (m = node_m >= 0): squarings + one reciprocal;
 // m < 0 (non-integer nu: an IFM-fitted copula) selects exp(ex log b) from log_node / exp_node
@@ -453,7 +450,6 @@ __device__ __forceinline__ double pow_node(double b, int m, double ex) {
         if (!(r < 1.0e300)) return r == r ? 0.0 : r;     // overflow -> 0, NaN stays NaN
         return fast_rcp(r);
     }
-    if (CVQ_POW_LIB) return exp(ex * log(b));
     return pow_gen(b, ex);                                   // ex <= -1/2: +inf -> 0, NaN stays NaN
 }
 

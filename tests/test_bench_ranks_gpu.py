@@ -25,9 +25,12 @@ def _port():
     return p
 
 
-def _bench(args, nproc):
+def _bench(args, nproc, self_launch=False):
     env = dict(os.environ, PYTHONUNBUFFERED="1")
-    if nproc == 1:
+    if self_launch:                                 # bench.py starts its own ranks (no launcher)
+        env.pop("WORLD_SIZE", None)
+        cmd = [sys.executable, "bench.py", "--gpus", str(nproc), "--backend", "gloo"]
+    elif nproc == 1:
         cmd = [sys.executable, "bench.py"]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -57,3 +60,12 @@ def test_two_ranks_weak_and_strong_match_one_rank():
     ss = strong["single_solve"]
     assert 0 < ss["local_solve_ms"] <= ss["ms_per_step"] * 1.5
     assert ss["allgather_finalize_ms"] >= 0.0
+
+
+def test_bench_gpus_flag_launches_its_own_ranks():
+    """`python3 bench.py --gpus 2` with no external launcher runs two ranks:
+    n_gpus 2 and the 1-rank VaR of the same 240 dates."""
+    one = _bench(COMMON + ["--dates-per-gpu", "240"], 1)
+    two = _bench(COMMON + ["--config", "2", "--dates-per-gpu", "120"], 2, self_launch=True)
+    assert two["n_gpus"] == 2 and two["config"]["global_dates"] == 240
+    assert two["var_checksum"] == one["var_checksum"], (two["var_checksum"], one["var_checksum"])

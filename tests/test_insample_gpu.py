@@ -146,3 +146,31 @@ def test_garch_forecast_pq_kernel_matches_reference_golden():
         w = z["params"][i][:1 + p + q]
         got = engine.garch_forecast_pq(s, n_in, int(p), int(q), w)
         np.testing.assert_allclose(got, z["forecasts"][i], rtol=1e-13, err_msg=f"GARCH({p},{q})")
+
+
+@pytest.mark.parametrize("device", [0, 1])
+def test_msm_adapter_marginals_run_on_its_device(device):
+    """the MSM adapter's in-sample marginals run on the adapter's device
+    (set_device), and the library restores the caller's current HIP device afterwards
+    (torch shares it)."""
+    import torch
+    from copula_var.insample import msm_marginals_densities
+    from copula_var.utils.calc_var_ABC import SharedCacheCopulaMSMVaR
+    from copula_var.utils.model_estimation.model.msm_estimation import MSMEstimation
+    if device >= torch.cuda.device_count():
+        pytest.skip(f"needs {device + 1} GPUs")
+    torch.cuda.set_device(0)
+    x = _mr_series(n=600, seed=9)[:, 0]
+    est = MSMEstimation()
+    est.device = device
+    prm = {"m_0": 0.6, "sig": float(np.std(x)), "b": 2.5, "gamma": 0.4}
+    key = ("dev_probe", "marginals_3")
+    SharedCacheCopulaMSMVaR.cache.pop(key, None)
+    try:
+        m, d, v = est.calculate_marginals_and_densities_in_sample({"dev_probe": x}, {"dev_probe": {"optimal_params": prm}}, 3)
+    finally:
+        SharedCacheCopulaMSMVaR.cache.pop(key, None)
+    assert torch.cuda.current_device() == 0
+    mh, dh, _ = msm_marginals_densities(x, 3, prm["m_0"], prm["sig"], prm["b"], prm["gamma"])
+    np.testing.assert_allclose(m[:, 0], mh, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(d[:, 0], dh, rtol=1e-12, atol=1e-300)

@@ -91,6 +91,10 @@ for i, nm in enumerate(names):
     print(f"  {nm:9s} mean {d[:, i].mean():9.0f}  max {d[:, i].max():9.0f}")
 slow = np.argsort(tot)[-max(1, T // 20):]        # slowest 5% of the workgroups
 print("slowest 5%: mean cycles by phase:", " ".join(f"{nm}={d[slow, i].mean():.0f}" for i, nm in enumerate(names)))
+if STRAT in ("sorted", "sweep") and T <= 16:      # dates alone on the GPU: per-date phases
+    for i in range(T):
+        print(f"  date {i}: nodes {int(nodes[i])} us {(rt[i, 1] - rt[i, 0]) / 100:.1f} phases "
+              + " ".join(f"{nm}={d[i, k]}" for k, nm in enumerate(names)))
 if STRAT != "direct":
     r0 = rt[:, 0] - rt[:, 0].min()
     r1 = rt[:, 1] - rt[:, 0].min()
