@@ -18,7 +18,7 @@ for p in (REPO, PKG_DIR):
         sys.path.insert(0, p)
 
 GOLDEN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN)
-                      if f.endswith(".npz") and f != "kat_special.npz" and not f.startswith("optim_"))
+                      if f.endswith(".npz") and f != "kat_special.npz" and not f.startswith(("optim_", "fullbatch_")))
 
 
 def pytest_configure(config):

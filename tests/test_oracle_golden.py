@@ -89,3 +89,44 @@ def test_q1_case_is_covered():
         b1 = z["call01_bounds"]
         seen |= {tuple(r) for r in np.round(b1, 6)}
     assert (-3.0, -2.0) in seen and (-3.5, -3.0) in seen
+
+
+def test_fullbatch_fixtures_are_consistent():
+    """The full-batch fixtures (gen_fullbatch.py) hold what the GPU tests compare against:
+    the whole batch, finite VaRs, the global iteration count of a solve without a Q4 break,
+    and the oracle's forecast tables for the first dates (re-derived here on the CPU)."""
+    import os
+    from conftest import GOLDEN
+    from copula_var import synthetic
+    from oracle import forecast as F
+    for cfg, T in ((2, 1000), (5, 5000), (3, 5000)):
+        path = os.path.join(GOLDEN, f"fullbatch_cfg{cfg}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        assert int(z["T"]) == T and z["var"].shape == (T,) and not np.isnan(z["var"]).any()
+        assert 19 <= int(z["iterations"]) <= 22 and not bool(z["broke"])
+        c = synthetic.baseline_configs()[cfg]
+        _, ptf, windows = F.insample_split(synthetic.simulate_returns(c)[:c.n_in + 4], c.n_in, c.weights)
+        assert ptf == float(z["ptf_mean"])
+        if c.model == "msm":
+            m = F.msm_integration_params(windows, c.msm_params, c.k, c.num_points)
+            np.testing.assert_array_equal(m["forecasts_by_states"], z["forecasts_by_states"][:4])
+        else:
+            np.testing.assert_array_equal(F.sigma_forecasts(windows, c.model, c.model_params()),
+                                          z["sigma_forecasts"][:4])
+
+
+def test_q4_zero_case_oracle():
+    """The constructed Q4 case (tests/q4_zero_case.py): the oracle breaks on the all-zero
+    iteration with the bracket midpoint, as the reference's loop does (calc_var_class.py:293)."""
+    from oracle.quadrature import Problem, calc_var
+    from q4_zero_case import CASES, build
+    for l22, (var_ref, it_ref) in CASES.items():
+        z = build(l22)
+        P = Problem(z["model"], z["copula"], 2, z["x_values"], z["step"], z["densities"], z["combos"],
+                    z["weights"], z["copula_params"], (z["forecasts_by_states"], z["forecasts"]),
+                    z["unique_vol_states"])
+        m = P.mass(0)
+        assert np.count_nonzero(m) == 4 and np.all(m[m != 0] == 2.0 ** -8)
+        var, it, broke = calc_var(P.compute_integral, P.T, z["ptf_mean"])
+        assert broke and it == it_ref
+        np.testing.assert_array_equal(var, np.full(P.T, var_ref))
