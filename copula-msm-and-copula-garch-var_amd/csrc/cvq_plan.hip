@@ -176,14 +176,13 @@ struct cvq_plan {
     double* d_svs = nullptr;     // [G]
     int* d_tree = nullptr;       // [4][1 << tree_depth]
     int tree_depth = 0;
-    int* d_sweep0 = nullptr;     // SWEEP: pass-0 boundary list
-    uint32_t* d_trw0 = nullptr;  // SWEEP: transposed node words of pass 0 / bracket 2's root pass
-    uint32_t* d_trw2 = nullptr;
+    int* d_pass = nullptr;       // SWEEP: both passes' boundary positions, then their child links
     std::vector<uint32_t> hidx;  // SORTED node words (host copy, v*-sorted)
     uint32_t* d_pidx = nullptr;  // solve-order copies of the node words / v* (row-major inside
     double* d_pvs = nullptr;     // each segment between slab ends; ensure_sorted_tree)
-    int sweep_d0 = 0, sweep_d = 0;
-    bool sweep_ok = false;       // SWEEP usable for the cached solve arguments (levels ordered)
+    int pass_ma = 0, pass_mb = 0;   // SWEEP: boundaries of pass A / B (0: the SORTED levels instead)
+    int pass_fix[kPassFix] = {0, 0, 0, 0, 0};
+    int pass_root[4] = {-1, -1, -1, -1};
     int layout = 0;              // SORTED node-word layout (sorted_pack)
     int fixpos[6] = {0, 0, 0, 0, 0, 0};
     std::vector<int> hcuts;      // solve-order segment ends (ensure_sorted_tree; cvq_plan_debug_cuts)
@@ -449,6 +448,94 @@ int host_ub(const std::vector<double>& vs, double v) {        // #{v* <= v}; NaN
     return (int)(std::upper_bound(vs.begin(), vs.end(), v) - vs.begin());
 }
 
+// SWEEP's pass tables (k_sorted<SWEEP>): pass A over (lower, sg1] = positions [fix0, fix3), pass B
+// over bracket 2's (sg1, vmax] = [fix3, fix5).  A pass's boundaries are its range ends, the fixed
+// levels inside it and the mids of its brackets' trees pruned to the cells holding more than
+// kPassCell nodes (a child is kept only under a kept parent, so a date's walk is a root path);
+// per boundary the boundary indices of its two children's mids.  Needs lower <= vmin <= sg0 <= fg
+// <= sg1 <= vmax (the solve's default levels); otherwise pass_ma = 0 and the solve runs SORTED's
+// levels.  Pruning is coarsened until both lists fit kPassMax.
+int build_pass_tables(cvq_plan* p, const SolveConst& P, const std::vector<int>& tree, int depth) {
+    p->pass_ma = p->pass_mb = 0;
+    for (int b = 0; b < 4; ++b) p->pass_root[b] = -1;
+    const bool ordered = P.lower <= P.vmin && P.vmin <= P.sg0 && P.sg0 <= P.fg && P.fg <= P.sg1 && P.sg1 <= P.vmax;
+    if (!ordered || p->S.dim != 2) return CVQ_OK;
+    const int* fp = p->fixpos;                            // lower, sg0, fg, sg1, vmin, vmax
+    const int bend[4][2] = {{fp[4], fp[1]}, {fp[1], fp[2]}, {fp[3], fp[5]}, {fp[2], fp[3]}};   // k_sorted's br
+    for (int cell = kPassCell; cell < (1 << 30); cell *= 2) {
+        // kept tree nodes per bracket: (heap node, position), pre-order
+        std::vector<std::pair<int, int>> kept[4];
+        for (int b = 0; b < 4; ++b) {
+            std::vector<int> stack{1};
+            std::vector<std::pair<int, int>> ends{{bend[b][0], std::max(bend[b][1], bend[b][0])}};
+            while (!stack.empty()) {
+                const int h = stack.back();
+                const std::pair<int, int> e = ends.back();
+                stack.pop_back();
+                ends.pop_back();
+                if (depth == 0 || h >= (1 << depth) || e.second - e.first <= cell) continue;
+                const int pm = std::min(std::max(tree[((size_t)b << depth) + h], e.first), e.second);
+                kept[b].emplace_back(h, pm);
+                stack.push_back(2 * h + 1);
+                ends.emplace_back(pm, e.second);
+                stack.push_back(2 * h);
+                ends.emplace_back(e.first, pm);
+            }
+        }
+        // entries (position, tag): tag -1 - e = fixed level e, else (b << 24) | heap node; positions may
+        // repeat (an empty slab), so every entry keeps its own index
+        std::vector<std::pair<int, int>> ea, eb;
+        const int fixv[kPassFix] = {fp[0], fp[4], fp[1], fp[2], fp[3]};
+        for (int e = 0; e < kPassFix; ++e) ea.emplace_back(fixv[e], -1 - e);
+        eb.emplace_back(fp[3], -1);
+        eb.emplace_back(std::max(fp[5], fp[3]), -2);
+        for (int b = 0; b < 4; ++b)
+            for (auto& k : kept[b]) (b == 2 ? eb : ea).emplace_back(k.second, (b << 24) | k.first);
+        if (ea.size() + eb.size() > (size_t)kPassMax) continue;
+        std::stable_sort(ea.begin(), ea.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+            return x.first < y.first;
+        });
+        std::stable_sort(eb.begin(), eb.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+            return x.first < y.first;
+        });
+        std::vector<int> la, lb, ca(ea.size(), 0), cb(eb.size(), 0);
+        std::vector<std::vector<int>> where(4, std::vector<int>((size_t)1 << std::max(depth, 0), -1));
+        for (size_t k = 0; k < ea.size(); ++k) {
+            la.push_back(ea[k].first);
+            if (ea[k].second < 0) p->pass_fix[-1 - ea[k].second] = (int)k;
+            else where[(size_t)(ea[k].second >> 24)][(size_t)(ea[k].second & 0xFFFFFF)] = (int)k;
+        }
+        for (size_t k = 0; k < eb.size(); ++k) {
+            lb.push_back(eb[k].first);
+            if (eb[k].second >= 0) where[2][(size_t)(eb[k].second & 0xFFFFFF)] = (int)k;
+        }
+        const int hn = depth > 0 ? (1 << depth) : 0;
+        for (int b = 0; b < 4; ++b) {
+            std::vector<int>& ch = b == 2 ? cb : ca;
+            const std::vector<int>& wb = where[(size_t)b];
+            p->pass_root[b] = kept[b].empty() ? -1 : wb[1];
+            for (auto& k : kept[b]) {
+                const int hh = k.first;
+                const int lft = 2 * hh < hn ? wb[(size_t)2 * hh] : -1;
+                const int rgt = 2 * hh + 1 < hn ? wb[(size_t)2 * hh + 1] : -1;
+                ch[(size_t)wb[(size_t)hh]] = (lft + 1) | ((rgt + 1) << 16);
+            }
+        }
+        std::vector<int> h;
+        h.insert(h.end(), la.begin(), la.end());
+        h.insert(h.end(), lb.begin(), lb.end());
+        h.insert(h.end(), ca.begin(), ca.end());
+        h.insert(h.end(), cb.begin(), cb.end());
+        if (int rc = dev_alloc(&p->d_pass, h.size())) return rc;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pass, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
+        CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));    // h is a local
+        p->pass_ma = (int)la.size();
+        p->pass_mb = (int)lb.size();
+        return CVQ_OK;
+    }
+    return CVQ_OK;
+}
+
 // ub() of the fixed levels and, per bracket, of the bisection mids down to the depth
 // where every cell holds <= sorted_tail_cap(dim) nodes (the device searches deeper levels).
 int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
@@ -518,7 +605,6 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
     auto row_key = [&](uint32_t c) {                           // (i1, a0, j): rows of the inner axis
         int a0, i1, j;
         if (lay == kLay2) { a0 = (int)(c & 0xFFFFu) >> 4; i1 = 0; j = ((int)(c >> 16) >> 4) - ns; }
-        else if (lay == kLay2W) { a0 = (int)(c & 0xFFFFu) >> 5; i1 = 0; j = ((int)(c >> 16) >> 5) - ns; }
         else if (lay == kLay3F) { a0 = (int)((c >> 4) & 0xFFu); i1 = (int)((c >> 12) & 0x7Fu); j = (int)(c >> 25); }
         else { a0 = (int)(c & 0x1FFu); i1 = (int)((c >> 9) & 0xFFu); j = (int)(c >> 17); }
         return ((long long)i1 << 40) | ((long long)a0 << 20) | (long long)j;
@@ -538,79 +624,6 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
             pvs[q] = vs[ord[q - c0].second];
         }
     }
-    if (p->strategy == CVQ_STRATEGY_SWEEP && (lay == kLay2 || lay == kLay2W)) {
-        // SWEEP's lanes read positions a chunk apart, not consecutive ones: inside each segment of
-        // the two root passes' ranges, pick for every (round, lane) the node whose two LDS records
-        // add the fewest bank-slot conflicts to its ds_read_b128 lane group (greedy, <= 64
-        // candidates per position).
-        auto group_of = [](int l) {                            // ds_read_b128 lane groups (MI355X_MICROARCH §LDS)
-            const int h = l >> 5, m = l & 31;
-            const int g = (m < 4 || (m >= 12 && m < 16) || (m >= 20 && m < 28)) ? 0 : 1;
-            return 2 * h + g;
-        };
-        auto seg_of = [&](int q) {
-            return (int)(std::upper_bound(cuts.begin(), cuts.end(), q) - cuts.begin()) - 1;
-        };
-        auto greedy = [&](int ps, int pe) {
-            if (pe - ps < 2) return;
-            int a0, L;
-            sweep_chunks(ps, pe, kSortNT, &a0, &L);
-            const int s0 = seg_of(ps), s1 = seg_of(pe - 1);
-            std::vector<std::vector<int>> pool((size_t)(s1 - s0 + 1));   // remaining positions (row-major order)
-            std::vector<char> keep((size_t)(s1 - s0 + 1), 0);
-            for (int sg = s0; sg <= s1; ++sg) {
-                const int c0 = std::max(cuts[sg], ps), c1 = std::min(cuts[sg + 1], pe);
-                bool searchable = false;
-                for (int b2 = 0; b2 < 4; ++b2)
-                    searchable |= cuts[sg + 1] - cuts[sg] > tcap && cuts[sg] >= bpos[b2][0] && cuts[sg + 1] <= bpos[b2][1];
-                keep[sg - s0] = searchable;
-                for (int q = c1 - 1; q >= c0; --q) pool[sg - s0].push_back(q);   // back = first in row order
-            }
-            std::vector<uint32_t> nidx(pidx.begin() + ps, pidx.begin() + pe);
-            std::vector<double> nvs(pvs.begin() + ps, pvs.begin() + pe);
-            const int shift = lay == kLay2W ? 5 : 4;
-            for (int r = 0; r < L / 4; ++r)
-                for (int u = 0; u < 4; ++u)
-                    for (int w = 0; w < kSortNT / 64; ++w) {
-                        std::vector<uint32_t> ra[4][16], ca[4][16];    // distinct record addresses per group / slot
-                        for (int l = 0; l < 64; ++l) {
-                            const int t = 64 * w + l, q = a0 + t * L + 4 * r + u;
-                            if (q < ps || q >= pe) continue;
-                            const int sg = seg_of(q) - s0, g = group_of(l);
-                            std::vector<int>& pl = pool[sg];
-                            int best = (int)pl.size() - 1;
-                            if (!keep[sg]) {
-                                int bscore = 1 << 30;
-                                for (int k = (int)pl.size() - 1, seen = 0; k >= 0 && seen < 64; --k, ++seen) {
-                                    const uint32_t c = pidx[pl[k]];
-                                    const uint32_t a1 = c & 0xFFFFu, a2 = c >> 16;
-                                    const std::vector<uint32_t>& v1 = ra[g][(a1 >> shift) & 15];
-                                    const std::vector<uint32_t>& v2 = ca[g][(a2 >> shift) & 15];
-                                    const int sc = (std::find(v1.begin(), v1.end(), a1) != v1.end() ? 0 : (int)v1.size()) +
-                                                   (std::find(v2.begin(), v2.end(), a2) != v2.end() ? 0 : (int)v2.size());
-                                    if (sc < bscore) { bscore = sc; best = k; if (sc == 0) break; }
-                                }
-                            } else {
-                                best = -1;                     // searchable: the position keeps its node
-                                for (int k = 0; k < (int)pl.size(); ++k) if (pl[k] == q) { best = k; break; }
-                            }
-                            const int src = pl[best];
-                            pl.erase(pl.begin() + best);
-                            const uint32_t c = pidx[src];
-                            nidx[q - ps] = c;
-                            nvs[q - ps] = pvs[src];
-                            std::vector<uint32_t>& v1 = ra[g][((c & 0xFFFFu) >> shift) & 15];
-                            std::vector<uint32_t>& v2 = ca[g][((c >> 16) >> shift) & 15];
-                            if (std::find(v1.begin(), v1.end(), c & 0xFFFFu) == v1.end()) v1.push_back(c & 0xFFFFu);
-                            if (std::find(v2.begin(), v2.end(), c >> 16) == v2.end()) v2.push_back(c >> 16);
-                        }
-                    }
-            std::copy(nidx.begin(), nidx.end(), pidx.begin() + ps);
-            std::copy(nvs.begin(), nvs.end(), pvs.begin() + ps);
-        };
-        greedy(p->fixpos[0], p->fixpos[3]);
-        greedy(p->fixpos[3], std::max(p->fixpos[5], p->fixpos[3]));
-    }
     pidx.resize(((pidx.size() + 3) & ~(size_t)3) + kSortIdxPad, 0u);
     if (int rc = dev_alloc(&p->d_pidx, pidx.size())) return rc;
     if (int rc = dev_alloc(&p->d_pvs, std::max<size_t>(pvs.size(), 1))) return rc;
@@ -619,51 +632,8 @@ int ensure_sorted_tree(cvq_plan* p, const SolveConst& P) {
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pvs, pvs.data(), pvs.size() * sizeof(double), hipMemcpyHostToDevice,
                                  p->stream));
     if (p->strategy == CVQ_STRATEGY_SWEEP) {
-        // pass 0 covers (lower, sg1] and needs lower <= vmin <= sg0 <= fg <= sg1 <= vmax
-        p->sweep_ok = P.lower <= P.vmin && P.vmin <= P.sg0 && P.sg0 <= P.fg && P.fg <= P.sg1 && P.sg1 <= P.vmax;
-        p->sweep_d0 = std::min(depth, kSweepD0Max);
-        p->sweep_d = std::min(std::max(depth, 1), kSweepDMax);
-        // in-order mids of bracket b's subtree of depth d0 (heap node (l, m) = entry (2m + 1) 2^(d0 - 1 - l) - 1)
-        const int d0 = p->sweep_d0, M0 = (1 << d0) - 1;
-        std::vector<int> l0((size_t)3 * M0 + 3, 0);
-        auto inorder = [&](int b, int o) {
-            for (int k = 0; k < M0; ++k) {
-                int l = d0 - 1, v = k + 1;
-                while (!(v & 1)) { v >>= 1; --l; }
-                const int m = (k + 1) >> (d0 - l);
-                l0[(size_t)o + k] = tree[((size_t)b << depth) + (1 << l) + m];
-            }
-        };
-        l0[0] = p->fixpos[4];                                  // vmin
-        inorder(0, 1);
-        l0[(size_t)M0 + 1] = p->fixpos[1];                     // sg0
-        inorder(1, M0 + 2);
-        l0[(size_t)2 * M0 + 2] = p->fixpos[2];                 // fg
-        inorder(3, 2 * M0 + 3);
-        for (size_t k = 1; k < l0.size() && p->sweep_ok; ++k) p->sweep_ok = l0[k - 1] <= l0[k];
-        if (int rc = dev_alloc(&p->d_sweep0, l0.size())) return rc;
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_sweep0, l0.data(), l0.size() * sizeof(int), hipMemcpyHostToDevice,
-                                     p->stream));
-        // node words of [ps, pe) in the sweep's chunk order: (thread t, round r, u) at (r NT + t) 4 + u
-        std::vector<uint32_t> trw0, trw2;
-        auto transpose = [&](int ps, int pe, std::vector<uint32_t>& out) {
-            int a0, L;
-            sweep_chunks(ps, pe, kSortNT, &a0, &L);
-            out.assign((size_t)kSortNT * std::max(L, 4), 0u);
-            for (int t = 0; t < kSortNT; ++t)
-                for (int k = 0; k < L; ++k) {
-                    const size_t pos = (size_t)a0 + (size_t)t * L + k;
-                    out[((size_t)(k / 4) * kSortNT + t) * 4 + k % 4] = pos < (size_t)G ? pidx[pos] : 0u;
-                }
-        };
-        transpose(p->fixpos[0], p->fixpos[3], trw0);
-        transpose(p->fixpos[3], std::max(p->fixpos[5], p->fixpos[3]), trw2);
-        if (int rc = dev_alloc(&p->d_trw0, trw0.size())) return rc;
-        if (int rc = dev_alloc(&p->d_trw2, trw2.size())) return rc;
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_trw0, trw0.data(), trw0.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                     p->stream));
-        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_trw2, trw2.data(), trw2.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                     p->stream));
+        int rc = build_pass_tables(p, P, tree, depth);
+        if (rc) return rc;
     }
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
     p->tree_depth = depth;
@@ -845,12 +815,13 @@ SortedGeom sorted_geom(const cvq_plan* p, bool solve) {
     G.G = (int)p->S.G;
     G.depth = p->tree_depth;
     for (int e = 0; e < 6; ++e) G.fix[e] = p->fixpos[e];
-    G.sweep0 = p->d_sweep0;
-    G.d0 = p->sweep_d0;
-    G.dsweep = p->sweep_d;
-    G.trw0 = p->d_trw0;
+    G.pass_bl = p->d_pass;
+    G.pass_ch = p->d_pass ? p->d_pass + p->pass_ma + p->pass_mb : nullptr;
+    G.pass_ma = solve ? p->pass_ma : 0;
+    G.pass_mb = p->pass_mb;
+    for (int e = 0; e < kPassFix; ++e) G.pass_fix[e] = p->pass_fix[e];
+    for (int b = 0; b < 4; ++b) G.pass_root[b] = p->pass_root[b];
     G.layout = p->layout;
-    G.trw2 = p->d_trw2;
     G.tidx = p->d_sidx;
     G.tvs = p->d_svs;
     return G;
@@ -868,7 +839,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         return launch_sorted(p->S, P, sorted_geom(p, true), p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi,
                              direct_fused(p), 0, nullptr, nullptr, snaps, hdr,
                              dbg_stamps ? (double*)p->d_stamps : nullptr,
-                             p->strategy == CVQ_STRATEGY_SWEEP && p->sweep_ok, kernel_abi_key() ^ (sizeof(SortedGeom) << 40));
+                             p->strategy == CVQ_STRATEGY_SWEEP && p->pass_ma > 0, kernel_abi_key() ^ (sizeof(SortedGeom) << 40));
     }
     if (p->strategy == CVQ_STRATEGY_COMPACT && p->S.n <= compact_max_n()) {
         int rc = ensure_cutfix(p, P);
@@ -1298,13 +1269,11 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     }
     if (sorted_family(p)) {                            // reachable nodes sorted by their exact threshold v*
         std::vector<uint32_t> idx;
-        // SWEEP + Student with an integer power: 32-B records with the folded scale (kLay2W)
-        p->layout = (p->strategy == CVQ_STRATEGY_SWEEP && sorted_fold(S.copula, S.dim, S.node_m))
-                  ? kLay2W : sorted_layout(S.dim, n);
+        p->layout = sorted_layout(S.dim, n);
         build_sorted_nodes(p->hx, S, kmax, p->layout, p->hvs, idx);
         const size_t nv = idx.size();
         p->hidx = idx;
-        idx.resize(((nv + 3) & ~(size_t)3) + kSortIdxPad, 0u);   // SWEEP / range-sum loads past the end
+        idx.resize(((nv + 3) & ~(size_t)3) + kSortIdxPad, 0u);   // range sums' / passes' loads past the end
         if ((rc = dev_alloc(&p->d_sidx, idx.size())) || (rc = dev_alloc(&p->d_svs, nv))) {
             cvq_plan_destroy(p);
             return rc;
@@ -1366,7 +1335,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
                     (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
-                    (void*)p->d_tree, (void*)p->d_sweep0, (void*)p->d_trw0, (void*)p->d_trw2,
+                    (void*)p->d_tree, (void*)p->d_pass,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);

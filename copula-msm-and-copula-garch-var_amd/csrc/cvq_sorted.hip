@@ -34,10 +34,9 @@ int device_cus() {
 // (625 dates: 384 threads, every workgroup resident) measured slower than 512 threads with the
 // last ~100 dates starting late (cfg 3 133 vs 116 us, cfg 5 118 vs 103 us; profiles/r04o).
 // CVQ_SORT_NT (256 / 384 / 512 / 1024) overrides (A/B).
-int sorted_threads(long long T, int dim, bool narrow) {
+int sorted_threads(long long T, int dim) {
     const char* ev = getenv("CVQ_SORT_NT");            // read per launch: tests switch it per case
     const int env = ev ? atoi(ev) : 0;
-    if (narrow) return kSortNT;
     if (env == 256 || env == 384 || env == 512 || env == 1024) return env;
     for (int nt = 1024; nt > kSortNT; nt >>= 1)
         if (T * (nt / 64) <= (long long)device_cus() * 4 * sorted_min_waves(dim, nt)) return nt;
@@ -52,8 +51,7 @@ int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, 
                 "libcvq objects built from different headers (rebuild all)");
     CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
     const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
-    // SWEEP solves and the folded SWEEP records (kLay2W) exist at 256 threads only
-    const int nt = sorted_threads(T, S.dim, (sweep && mode == 0) || G.layout == kLay2W);
+    const int nt = sorted_threads(T, S.dim);
     switch (nt) {
         case 1024: sorted_slice_1024(L); break;
         case 512: sorted_slice_512(L); break;

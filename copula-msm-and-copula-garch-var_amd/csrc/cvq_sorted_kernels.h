@@ -50,7 +50,7 @@ constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisec
 #define CVQ_SORT_ILP 4
 #endif
 // zero words after the node lists: a range sum's prefetch reads up to one round (kSortIlp x the
-// widest workgroup) past its range, SWEEP's 16-B loads up to 4 words
+// widest workgroup) past its range
 constexpr int kSortIdxPad = CVQ_SORT_ILP * 1024;
 constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
 #ifndef CVQ_SORT_ILP_GEN
@@ -71,15 +71,19 @@ __host__ __device__ constexpr int sorted_ilp(int cop, int pm, int dim, int nt = 
          : (cop == CVQ_STUDENT && nt >= 512) ? CVQ_SORT_ILP_WIDE_ST : kSortIlp;
 }
 
-// SWEEP (2-D): boundary list capacity per pass (LDS, double-buffered), the depth of the
-// pass-0 subtrees (3 (2^d0 - 1) + 3 <= cap) and of a later pass's subtree (2^d - 1 <= cap).
 constexpr int kSortNT = 256;                          // threads per k_sorted workgroup
-#ifndef CVQ_SWEEP_MIN_WAVES
-#define CVQ_SWEEP_MIN_WAVES 4                         // SWEEP: <= 128 VGPRs (the pass loop holds the solve state)
-#endif
-constexpr int kSweepCap = 256;
-constexpr int kSweepD0Max = 6;
-constexpr int kSweepDMax = 8;
+
+// SWEEP (2-D): the first bisection levels from ONE pass over each bracket group's
+// nodes.  Pass A covers (lower, sg1] (r0, both second slabs, brackets 0, 1 and 3), pass B bracket
+// 2's (sg1, vmax]; a pass records the prefix sum at every boundary of its list -- the fixed
+// levels and the mids of the bracket trees' cells holding more than kPassCell nodes (host-pruned
+// trees) -- and the levels below those cells run as SORTED's.  kPassMax bounds both lists.
+constexpr int kPassCell = 1024;
+constexpr int kPassMax = 512;
+constexpr int kPassFix = 5;
+#ifndef CVQ_PASS_ILP
+#define CVQ_PASS_ILP 2                                // steps in flight per wave of a pass
+#endif                           // pass A's boundaries of lower, vmin, sg0, fg, sg1
 
 // Date-independent device tables of a SORTED plan.
 struct SortedGeom {
@@ -91,28 +95,20 @@ struct SortedGeom {
     int G;
     int depth;
     int fix[6];            // ub() of lower, sg0, fg, sg1, vmin, vmax
-    // SWEEP: pass 0 covers (lower, sg1]; its sorted boundary list is ub() of vmin, the
-    // in-order mids of bracket 0's tree (depth d0), sg0, bracket 1's mids, fg, bracket 3's mids
-    const int* sweep0;     // [3 (2^d0 - 1) + 3]
-    int d0;                // pass-0 subtree depth
-    int dsweep;            // subtree depth of a later pass
-    // the node words of pass 0's range [fix0, fix3) and of bracket 2's [fix3, fix5) in the
-    // sweep's chunk order, transposed so a wave's round is one coalesced 1-KB load:
-    // word (thread t, round r, u) at [(r NT + t) 4 + u] (sweep_transpose)
-    const uint32_t* trw0;
-    const uint32_t* trw2;
-    int layout;            // node-word layout (sorted_pack): kLay2W for folded Student records
+    // SWEEP: pass A's then pass B's sorted boundary positions, and per boundary the packed
+    // boundary indices of its two child cells' mids in the pruned trees ((left + 1) | (right + 1) << 16,
+    // 0 = not subdivided); pass_root[b]: boundary index of bracket b's root mid (-1: none)
+    const int* pass_bl;    // [pass_ma + pass_mb]
+    const int* pass_ch;    // [pass_ma + pass_mb]
+    int pass_ma, pass_mb;
+    int pass_fix[kPassFix];
+    int pass_root[4];
+    int layout;            // node-word layout (sorted_pack)
     // the v*-sorted node words and v* (the solve order above is row-major inside each segment
     // between slab ends; the tail's prefix scan needs the tail cell's nodes in v* order)
     const uint32_t* tidx;
     const double* tvs;
 };
-
-// chunk geometry of a sweep over sorted positions [ps, pe): thread t takes [a0 + t L, a0 + (t + 1) L)
-__host__ __device__ inline void sweep_chunks(int ps, int pe, int nt, int* a0, int* L) {
-    *a0 = ps & ~3;
-    *L = ((pe - *a0 + 4 * nt - 1) / (4 * nt)) * 4;
-}
 
 // exp_node: cvq_special.h (the fast records clamp their logs at kLogFloor, within its domain)
 constexpr double kLogFloor = -1.0e4;
@@ -157,18 +153,7 @@ __device__ __forceinline__ int sorted_ub(const double* __restrict__ vs, int lo, 
 //           i1 in bits 12-18 (32-B axis-1 records), j in bits 25-31 (j * 16)
 //   kLay3G  (3-D, n <= 255): a0 | i1 << 9 | j << 17, record indices
 // with a0 = i0 + n on the plane i1 == 0 (Q6), whose axis-0 records are separate.
-//   kLay2W  (2-D, SWEEP Student with an integer power): as kLay2 with 32-B records holding the
-//           folded scale, off0 = 32 i0, off2 = 32 (ns + j) (see node_fast)
-enum { kLay2 = 0, kLay3F = 1, kLay3G = 2, kLay2W = 3 };
-// the plans whose SWEEP solve uses kLay2W: 2-D Student with nu = 6 (b^-4, the launcher's PM = 8)
-__host__ __device__ constexpr bool sorted_fold(int copula, int dim, int node_m) {
-    return copula == CVQ_STUDENT && dim == 2 && node_m == dim + 6;
-}
-__host__ __device__ constexpr double pow2_constexpr(int e) {
-    double r = 1.0;
-    for (int k = 0; k < e; ++k) r *= 2.0;
-    return r;
-}
+enum { kLay2 = 0, kLay3F = 1, kLay3G = 2 };
 constexpr int kLay3FMaxN = 128;
 constexpr int kLay3FAx1 = 4096, kLay3FAx2 = 8192, kLay3FBytes = 10240;   // byte offsets / size of its region
 __host__ __device__ constexpr int sorted_layout(int dim, int n) {
@@ -176,9 +161,8 @@ __host__ __device__ constexpr int sorted_layout(int dim, int n) {
 }
 inline uint32_t sorted_pack(int layout, int n, int i0, int i1, int j) {
     const int ns = (n + 1) & ~1;
-    const int a0 = i0 + (layout != kLay2 && layout != kLay2W && i1 == 0 ? n : 0);
+    const int a0 = i0 + (layout != kLay2 && i1 == 0 ? n : 0);
     if (layout == kLay2) return (uint32_t)(16 * i0) | ((uint32_t)(16 * (ns + j)) << 16);
-    if (layout == kLay2W) return (uint32_t)(32 * i0) | ((uint32_t)(32 * (ns + j)) << 16);
     if (layout == kLay3F) return ((uint32_t)a0 << 4) | ((uint32_t)i1 << 12) | ((uint32_t)j << 25);
     return (uint32_t)a0 | ((uint32_t)i1 << 9) | ((uint32_t)j << 17);
 }
@@ -200,10 +184,6 @@ __device__ __forceinline__ void unpack_node(uint32_t c, int ns, int* a0, int* i1
         *a0 = (int)(c & 0xFFFFu) >> 4;
         *i1 = 0;
         *j = ((int)(c >> 16) >> 4) - ns;
-    } else if constexpr (LAY == kLay2W) {
-        *a0 = (int)(c & 0xFFFFu) >> 5;
-        *i1 = 0;
-        *j = ((int)(c >> 16) >> 5) - ns;
     } else if constexpr (LAY == kLay3F) {
         *a0 = (int)__builtin_amdgcn_ubfe(c, 4, 8);
         *i1 = (int)__builtin_amdgcn_ubfe(c, 12, 7);
@@ -227,13 +207,13 @@ inline int sorted_stride(int n) { return (n + 1) & ~1; }
 // doubles of the table region
 __host__ __device__ inline int sorted_region_doubles(int layout, int n) {
     const int ns = (n + 1) & ~1;
-    return layout == kLay2 ? 6 * ns : layout == kLay2W ? 8 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
+    return layout == kLay2 ? 6 * ns : layout == kLay3F ? kLay3FBytes / 8 : 9 * ns;
 }
 constexpr int kSortScalars = 4;                // flags, arest, last (+ pad), after the reduction slots
 inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false, int layout = -1) {
     if (layout < 0) layout = sorted_layout(dim, n);
-    // SWEEP: scan slots [NT / 64] + prefix values [2][cap] + boundary positions [2][cap]
-    const size_t sw = sweep ? sizeof(double) * ((size_t)nt / 64 + 2 * kSweepCap) + sizeof(int) * 2 * kSweepCap : 0;
+    // SWEEP: wave-total slots [NT / 64] + per boundary its prefix value, position and children
+    const size_t sw = sweep ? sizeof(double) * ((size_t)nt / 64 + kPassMax) + sizeof(int) * 2 * kPassMax : 0;
     return sizeof(double) * ((size_t)sorted_region_doubles(layout, n) + 2 * (nt / 64) + kSortScalars) +
            sizeof(double2) * sorted_tail_cap(dim) + sw;
 }
@@ -263,15 +243,15 @@ __host__ __device__ constexpr int sorted_min_waves(int dim, int nt = 256, int co
                     : CVQ_SORT_MIN_WAVES3;
 }
 
-// SWEEP (2-D): instead of one strided range sum + one workgroup reduction per
-// bisection level, a pass evaluates every node of a cell once -- thread tid sums a contiguous
-// chunk of sorted positions in order -- recording the running sum at each sorted boundary
-// position of the cell's bisection subtree; one scan of the thread totals turns those into
-// prefix sums, and every thread then walks the subtree's levels from LDS (slab = difference of
-// two prefixes) with no further barrier.  Pass 0 covers (lower, sg1], so r0, the second slab
-// and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes one more.
+// SWEEP (2-D): the fixed slabs and the first bisection levels come from one pass
+// per bracket group instead of one strided range sum + one workgroup reduction per level: a
+// pass evaluates every node of its range once, each wave a contiguous run of 64-position steps,
+// recording the prefix sum at every boundary of its (host-pruned) list; every thread then walks
+// those levels from LDS (slab = difference of two prefixes) with no further barrier, and the
+// levels below the pruned trees run as SORTED's.  Pass A covers (lower, sg1], so r0, the second
+// slab and brackets 0, 1, 3 need no other pass; bracket 2 (sg1, vmax] takes pass B.
 template <int COP, bool MSM, int DIM, int NT, int PM, bool FUSED, int LAY, bool SWEEP = false>
-__global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(DIM, NT, COP, PM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
+__global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sorted(StaticDev S, SolveConst P, SortedGeom G, const double* __restrict__ a,
                                                const double* __restrict__ tA, const double* __restrict__ tB,
                                                const double* __restrict__ pi, int mode,
                                                const double* __restrict__ bounds, double* __restrict__ out,
@@ -291,7 +271,7 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     double* wg = Bg + DIM * ns;                    // generic [DIM][n]
     double* fr0 = lds;                             // fast [ns (3-D: 2 ns)][2] axis 0
     // axis 1 (3-D): kLay3F 32-B records (c01 z1, c12 z1, g1 | z1, B'1); kLay3G [ns][2] + fg1 [ns]
-    double* fr1 = LAY == kLay3F ? lds + kLay3FAx1 / 8 : fr0 + (DIM == 3 || LAY == kLay2W ? 4 : 2) * ns;
+    double* fr1 = LAY == kLay3F ? lds + kLay3FAx1 / 8 : fr0 + (DIM == 3 ? 4 : 2) * ns;
     double* fg1 = LAY == kLay3F ? fr1 + 2 : fr1 + (DIM == 3 ? 2 : 0) * ns;
     constexpr int R1 = LAY == kLay3F ? 4 : 2;      // doubles per axis-1 record
     constexpr int FG = LAY == kLay3F ? 4 : 1;      // fg1 stride
@@ -301,9 +281,10 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
     int& flags = *(int*)(red + 2 * (NT / 64));     // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
     double& s_arest = *(red + 2 * (NT / 64) + 1);  // 3-D: the axis-0 weight off the plane i1 == 0
     int& last = *(int*)(red + 2 * (NT / 64) + 2);  // fused finalize: this workgroup is the last
-    double* sred = red + 2 * (NT / 64) + kSortScalars;   // SWEEP: [NT / 64] scan slots
-    double* Pvs = sred + NT / 64;                  // SWEEP: [2][kSweepCap] prefix values
-    int* Bls = (int*)(Pvs + 2 * kSweepCap);        // SWEEP: [2][kSweepCap] boundary positions
+    double* sred = red + 2 * (NT / 64) + kSortScalars;   // SWEEP: [NT / 64] wave totals
+    double* Pvs = sred + NT / 64;                  // SWEEP: [kPassMax] prefix values (pass A, then B)
+    int* Bls = (int*)(Pvs + kPassMax);             // SWEEP: [kPassMax] boundary positions
+    int* Chs = Bls + kPassMax;                     // SWEEP: [kPassMax] packed child boundaries
 
     // diagnostic phase stamps (CVQ_STAMPS=1, never in a timed run): COMPACT's slots --
     // 0 start, 1 tables, 2 first slab, 3 second slab, 4 bracket, 5 + level, 29 tail
@@ -379,8 +360,11 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         s_arest = s0;
     }
     if (tid == 0 && lds_base(lds) != 0) bad |= 4;          // packed offsets need the region at LDS 0
-    if constexpr (SWEEP) {                                 // pass 0's boundary list -> buffer 0
-        for (int k = tid; k < 3 * ((1 << G.d0) - 1) + 3; k += NT) Bls[k] = G.sweep0[k];
+    if constexpr (SWEEP) {                                 // both passes' boundary lists -> LDS
+        for (int k = tid; k < G.pass_ma + G.pass_mb; k += NT) {
+            Bls[k] = G.pass_bl[k];
+            Chs[k] = G.pass_ch[k];
+        }
     }
     if (bad) atomicOr(&flags, bad);
     __syncthreads();
@@ -426,20 +410,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 fr1[R1 * i + 1] = k12 * z;
                 fg1[FG * i] = lg(B * w) + kcc;
             }
-        } else if (LAY == kLay2W) {                        // Student, folded scale s = sc^(-2/m)
-            const double sc = (ax == 0 ? S.term1 : 1.0) * B * w;
-            const double sf = PM == 8 ? 1.0 / sqrt(sqrt(sc)) : pow(sc, -2.0 / (PM > 0 ? PM : 1));
-            double* r = ax == 0 ? fr0 + 4 * i : fr2 + 4 * i;
-            if (ax == 0) {                                 // b' = X . Y = s0 s2 (1 + z^T R^-1 z / nu)
-                r[0] = sf * fma(kq * S.Ri[0], z * z, 1.0);
-                r[1] = sf * (k02 * z);
-                r[2] = sf;
-            } else {
-                r[0] = sf;
-                r[1] = sf * z;
-                r[2] = sf * (kq * S.Ri[3] * (z * z));
-            }
-            r[3] = 0.0;
         } else if constexpr (COP == CVQ_PLACKETT) {       // rec0 = (-2 u, theta s), rec2 = ((theta - 1) v, s)
             double* r = ax == 0 ? fr0 + 2 * i : fr2 + 2 * i;
             r[0] = ax == 0 ? -2.0 * z : (S.theta - 1.0) * z;
@@ -467,7 +437,7 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         return make_double2(v.x, v.y);
     };
     auto rec0 = [&](uint32_t c) -> const lds_f64* {
-        if constexpr (LAY == kLay2 || LAY == kLay2W) return lds_at(c & 0xFFFFu);
+        if constexpr (LAY == kLay2) return lds_at(c & 0xFFFFu);
         else if constexpr (LAY == kLay3F) return lds_at(c & 0xFF0u);
         else return lds_at(lds_base(fr0) + 16 * __builtin_amdgcn_ubfe(c, 0, 9));
     };
@@ -476,11 +446,10 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         else return lds_at(lds_base(fr1) + 16 * __builtin_amdgcn_ubfe(c, 9, 8));
     };
     auto rec2 = [&](uint32_t c) -> const lds_f64* {
-        if constexpr (LAY == kLay2 || LAY == kLay2W) return lds_at(c >> 16);
+        if constexpr (LAY == kLay2) return lds_at(c >> 16);
         else if constexpr (LAY == kLay3F) return lds_at(kLay3FAx2 + (c >> 21));
         else return lds_at(lds_base(fr2) + 16 * (c >> 17));
     };
-    constexpr double kFoldClamp = pow2_constexpr(2000 / (PM > 0 ? PM : 2000));
     // Plackett node (plackett.py:66-69, Q11) from the records (-2 u, theta s0), (a1 v, s2),
     // a1 = theta - 1: P = 1 + a1 (u + v), num / theta = 1 + a1 (u + v - 2 u v) = P + (-2 u)(a1 v),
     // denominator (P (theta + 1 - P))^2 -- 12 FP64 operations and one reciprocal a node: v_rcp_f64
@@ -497,17 +466,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         y = den == 0.0 ? __builtin_inf() : y;             // num / 0 as IEEE division gives it (num * inf)
         return (num * y) * (A.y * C.y);
     };
-    // 2-D node from its two 16-B records (kLay2): the sweep issues a round's LDS reads first
-    auto node2 = [&](const double2 A, const double2 C) -> double {
-        if constexpr (COP == CVQ_GAUSSIAN) {
-            return exp_node(fma(A.x, C.x, A.y + C.y));
-        } else if constexpr (COP == CVQ_STUDENT) {
-            const double b = fma(A.x, fma(a00, A.x, k02 * C.x), fma(a22 * C.x, C.x, 1.0));
-            return (A.y * C.y) * pow_fast<PM>(b, S.node_m, S.node_ex);
-        } else {
-            return plackett(A, C);
-        }
-    };
     auto node_fast = [&](uint32_t c) -> double {
         const double2 A = rd2(rec0(c));
         const double2 C = rd2(rec2(c));
@@ -520,15 +478,6 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
                 const double g1 = LAY == kLay3F ? r1[2] : fg1[__builtin_amdgcn_ubfe(c, 9, 8)];
                 return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
             }
-        } else if constexpr (COP == CVQ_STUDENT && LAY == kLay2W) {
-            // node = sc0 sc2 b^(-m/2) = b'^(-m/2), b' = s0 s2 b = X0 Y0 + X1 Y1 + X2 Y2 (records
-            // hold s = sc^(-2/m)); b' is clamped below 2^(2000/m) so b'^(m/2) stays finite
-            // (the node is then < 2^-1000 instead of its denormal / zero value)
-            const lds_f64* ra = rec0(c);
-            const lds_f64* rc = rec2(c);
-            const double2 X = rd2(ra), Y = rd2(rc);
-            const double b = fmin(fma(X.x, Y.x, fma(X.y, Y.y, ra[2] * rc[2])), kFoldClamp);
-            return pow_fast<PM>(b, S.node_m, S.node_ex);
         } else if constexpr (COP == CVQ_STUDENT) {
             double b, sc;
             if constexpr (DIM == 2) {
@@ -677,116 +626,84 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         return v == P.lower ? G.fix[0] : v == P.sg0 ? G.fix[1] : v == P.fg ? G.fix[2]
              : v == P.sg1 ? G.fix[3] : v == P.vmin ? G.fix[4] : G.fix[5];
     };
-    // SWEEP pass: the nodes at sorted positions [ps, pe) summed once, thread tid taking the
-    // contiguous chunk [s, s + L) (L a multiple of 4, chunks aligned to 4 positions: one
-    // 16-B index load per 4 nodes) in position order; Pv[i] = sum of the nodes before sorted
-    // position Bl[i] (Bl sorted, ps <= Bl[i] <= pe).  Returns the cell total; ends with a barrier.
-    auto sweep = [&](int ps, int pe, const int* Bl, double* Pv, int M, const uint32_t* trw) -> double {
-        int a0, L;
-        sweep_chunks(ps, pe, NT, &a0, &L);
-        const int s = a0 + tid * L, e = min(s + L, pe);
-        const int eown = tid == NT - 1 ? 0x7FFFFFFF : s + L;   // boundaries in [s, eown) are mine
+    // SWEEP pass: the nodes at sorted positions [ps, pe) summed once.  Wave w takes a contiguous
+    // run of 64-position steps from ps rounded down to 64 (lane = position mod 64, the lanes of a
+    // step reading consecutive positions as SORTED's range sums do), ILP steps per round with the
+    // next round's node words in flight; each lane keeps a running sum.  At a step holding
+    // boundaries (wave-uniform test) the wave reduces, per boundary, the running sums plus the
+    // step's values below it: the wave's partial prefix.  The wave totals' exclusive scan then
+    // turns partials into Pv[k] = sum of the nodes at [ps, Bl[k]) for every boundary k (ps <= Bl[k]
+    // <= pe, sorted).  Returns the total; ends with a barrier.
+    auto pass = [&](int ps, int pe, const int* Bl, double* Pv, int M) -> double {
+        constexpr int W = NT / 64;
+        constexpr int PILP = ILP < CVQ_PASS_ILP ? ILP : CVQ_PASS_ILP;
+        const int wv = tid >> 6;
+        const int a0 = ps & ~63;
+        const int nsteps = (max(pe, a0) - a0 + 63) >> 6;
+        const int spw = (nsteps + W - 1) / W;              // steps per wave
+        const int rs = a0 + wv * spw * 64;                 // this wave's positions [rs, re)
+        const int re = wv == W - 1 ? 0x7FFFFFFF : rs + spw * 64;
+        const int nst = max(0, min(spw, nsteps - wv * spw));
         int i = 0;
-        for (int hiI = M; i < hiI;) {                      // first boundary >= s
+        for (int hiI = M; i < hiI;) {                      // first boundary >= rs (wave-uniform)
             const int md = (i + hiI) >> 1;
-            if (Bl[md] < s) i = md + 1; else hiI = md;
+            if (Bl[md] < rs) i = md + 1; else hiI = md;
         }
         const int i0 = i;
-        int nb = i < M ? Bl[i] : 0x7FFFFFFF;             // my next boundary, and the one after it
-        int nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;     // (loaded a boundary ahead: no LDS wait in the loop)
-        double acc = 0.0;
-        if (fast) {
-            // node words: the root passes read a transposed copy (one coalesced 1-KB load per
-            // wave and round); deeper passes the solve order (a lane's chunk is its own lines)
-            auto word4 = [&](int p) {                      // the 4 node words of the round at position p
-                return trw ? ((const uint4*)trw)[tid + (size_t)((p - s) >> 2) * NT] : *(const uint4*)(G.idx + p);
-            };
-            // a round's 4 node values: every LDS read issued before the arithmetic
-            auto vals = [&](const uint4 w, double (&v)[4]) {
-                const uint32_t c[4] = {w.x, w.y, w.z, w.w};
-                if constexpr (LAY == kLay2) {
-                    double2 A[4], C[4];
+        int nb = i < M ? Bl[i] : 0x7FFFFFFF;
+        double run = 0.0;
+        auto sweep_steps = [&](auto nodef, auto ilp) {
+            constexpr int PI = decltype(ilp)::value;
+            const uint32_t* ip = G.idx + rs + lane;
+            uint32_t cn[PI];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        A[u] = rd2(rec0(c[u]));
-                        C[u] = rd2(rec2(c[u]));
+            for (int u = 0; u < PI; ++u) cn[u] = ip[u * 64];
+            for (int st = 0; st < nst; st += PI) {
+                uint32_t c[PI];
+#pragma unroll
+                for (int u = 0; u < PI; ++u) c[u] = cn[u];
+                ip += PI * 64;                            // the lists carry kSortIdxPad zero words
+#pragma unroll
+                for (int u = 0; u < PI; ++u) cn[u] = ip[u * 64];
+                double v[PI];
+#pragma unroll
+                for (int u = 0; u < PI; ++u) {
+                    const int q = rs + (st + u) * 64 + lane;
+                    const double x = nodef(c[u]);
+                    v[u] = (q >= ps && q < pe) ? x : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < PI; ++u) {
+                    if (st + u >= nst) break;
+                    const int sb = rs + (st + u) * 64;
+                    while (nb < sb + 64) {                 // boundaries inside this step (rare)
+                        const double part = wave_sum(run + ((lane < nb - sb) ? v[u] : 0.0));
+                        if (lane == 0) Pv[i] = part;
+                        ++i;
+                        nb = i < M ? Bl[i] : 0x7FFFFFFF;
                     }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = node2(A[u], C[u]);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = node_fast(c[u]);
+                    run += v[u];
                 }
-            };
-            // add a round's values in position order, recording the running sum at my boundaries
-            // in it (a boundary's prefix is exactly the running sum the later rounds continue)
-            auto round_add = [&](int p, const double (&v)[4]) {
-                const double s1 = acc + v[0], s2 = s1 + v[1], s3 = s2 + v[2];
-                while (nb < p + 4) {                       // divergent but short: no loads waited on
-                    const int off = nb - p;
-                    Pv[i] = off == 0 ? acc : off == 1 ? s1 : off == 2 ? s2 : s3;
-                    ++i;
-                    nb = nb2;
-                    nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
-                }
-                acc = s3 + v[3];
-            };
-            auto partial = [&](int p) {                    // a round with positions outside [ps, pe)
-                double v[4];
-                vals(word4(p), v);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = (p + u >= ps && p + u < pe) ? v[u] : 0.0;
-                round_add(p, v);
-            };
-            int p = s;
-            if (p < e && p < ps) {                         // thread 0's first round (ps not 4-aligned)
-                partial(p);
-                p += 4;
             }
-            uint4 wn = p + 4 <= e ? word4(p) : make_uint4(0u, 0u, 0u, 0u);
-            for (; p + 4 <= e; p += 4) {                   // full rounds; the next round's words in flight
-                const uint4 w = wn;
-                if (p + 8 <= e) wn = word4(p + 4);
-                double v[4];
-                vals(w, v);
-                round_add(p, v);
-            }
-            if (p < e) partial(p);                         // the last active thread's last round
-        } else {                                           // reference-semantics nodes, one at a time
-            for (int p = max(s, ps); p < e; ++p) {
-                while (nb == p) {
-                    Pv[i] = acc;
-                    ++i;
-                    nb = nb2;
-                    nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
-                }
-                acc += node_generic(G.idx[p]);
-            }
-        }
-        while (nb < eown) {                                // boundaries past my last node
-            Pv[i] = acc;
+        };
+        if (fast) sweep_steps(node_fast, std::integral_constant<int, PILP>());
+        else sweep_steps(node_generic, std::integral_constant<int, 1>());   // reference-semantics nodes one at a time
+        const double wt = wave_sum(run);
+        while (nb < re) {                                  // boundaries past my last step (pe, or empty steps)
+            if (lane == 0) Pv[i] = wt;
             ++i;
-            nb = nb2;
-            nb2 = i + 1 < M ? Bl[i + 1] : 0x7FFFFFFF;
+            nb = i < M ? Bl[i] : 0x7FFFFFFF;
         }
-        // exclusive scan of the thread totals (fixed order: identical in every thread)
-        double x = acc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        const double xe = __shfl_up(x, 1, 64);
-        if (lane == 63) sred[tid >> 6] = x;
+        if (lane == 0) sred[wv] = wt;
         __syncthreads();
-        double base = lane == 0 ? 0.0 : xe, total = 0.0;
+        double base = 0.0, total = 0.0;
 #pragma unroll
-        for (int w = 0; w < NT / 64; ++w) {
+        for (int w = 0; w < W; ++w) {
             const double sw = sred[w];
-            if (w < (tid >> 6)) base += sw;
+            if (w < wv) base += sw;
             total += sw;
         }
-        for (int k = i0; k < i; ++k) Pv[k] += base;
+        for (int k = i0 + lane; k < i; k += 64) Pv[k] += base;
         __syncthreads();
         return total;
     };
@@ -829,75 +746,56 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         prevU = mid;
         return ustack;
     };
+    bool passed = false;                                   // SWEEP: the passes gave the first levels
     if constexpr (SWEEP) {
-        // Passes share one code instance (register pressure): pass 0 covers (lower, sg1] with
-        // the fixed levels and brackets 0, 1, 3's subtrees; later passes one cell of the bracket.
-        const int M0 = (1 << G.d0) - 1;
-        int ps = G.fix[0], pe = G.fix[3], M = 3 * M0 + 3, buf = 0, npass = 0;
-        int* Bl = Bls;
-        double* Pv = Pvs;
-        const uint32_t* trw = G.trw0;
-        while (true) {
-            const double tot = sweep(ps, pe, Bl, Pv, M, trw);
-            if (npass < 3) stamp(npass == 0 ? 2 : 3 + 3 * npass);
-            nodes += pe - ps;
-            int o = 0, Ds = 0;
-            double Plo = 0.0, Phi = tot;
-            if (npass == 0) {
-                const double Pvmin = Pv[0], Psg0 = Pv[M0 + 1], Pfg = Pv[2 * M0 + 2];
-                const double r0 = Pfg;                     // (lower, fg]
-                const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-                const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
-                bracket(r0, nl, nu, (nl == P.fg) ? tot - Pfg : Pfg - Psg0);   // (fg, sg1] or (sg0, fg]
-                if (br == 0) { o = 1; Ds = G.d0; Plo = Pvmin; Phi = Psg0; }
-                if (br == 1) { o = M0 + 2; Ds = G.d0; Plo = Psg0; Phi = Pfg; }
-                if (br == 3) { o = 2 * M0 + 3; Ds = G.d0; Plo = Pfg; Phi = tot; }
-            } else {
-                Ds = M == 0 ? 0 : 31 - __builtin_clz(M + 1);
-            }
-            // the subtree's levels from LDS: heap node (level l, path m) is entry (2m + 1) 2^(Ds - 1 - l) - 1
-            for (int l = 0, m = 0; l < Ds && it < P.K && phi - plo > TCAP; ++l, ++it) {
-                const double mid = (lo + hi) / 2;
-                if (tid == 0) sn[it] = mid;
-                if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-                const int ii = o + ((2 * m + 1) << (Ds - 1 - l)) - 1;
-                const int pm = Bl[ii];
-                const double Pm = Pv[ii];
-                if (level(mid, ustack ? Pm - Plo : Phi - Pm)) { lo = mid; plo = pm; Plo = Pm; m = 2 * m + 1; }
-                else                                         { hi = mid; phi = pm; Phi = Pm; m = 2 * m; }
-                h = 2 * h + (ustack ? 1 : 0);
-            }
-            if (npass < 3) stamp(npass == 0 ? 3 : 4 + 3 * npass);
-            ++npass;
-            if (!(it < P.K && phi - plo > TCAP && h < tsz)) break;
-            // next pass: the cell (lo, hi] with its subtree of depth Ds (tabulated heap nodes only)
-            const int nDs = min(G.dsweep, G.depth - (31 - __builtin_clz(h)));
-            M = (1 << nDs) - 1;
-            buf ^= 1;
-            Bl = Bls + buf * kSweepCap;
-            Pv = Pvs + buf * kSweepCap;
-            for (int k = tid; k < M; k += NT) {             // in-order entry k -> heap node
-                const int l = nDs - 1 - __builtin_ctz(k + 1), m = (k + 1) >> (nDs - l);
-                Bl[k] = tr[(h << l) + m];
-            }
-            ps = plo;
-            pe = phi;
-            trw = (h == 1 && br == 2) ? G.trw2 : nullptr;
-            __syncthreads();
+      if (G.pass_ma > 0) {
+        passed = true;
+        // pass A over (lower, sg1]: r0 = I(lower, fg], both candidate second slabs and the pruned
+        // trees of brackets 0, 1, 3 (its list holds lower, vmin, sg0, fg, sg1 at pass_fix[])
+        const double totA = pass(G.fix[0], G.fix[3], Bls, Pvs, G.pass_ma);
+        (void)totA;
+        stamp(2);
+        nodes += max(G.fix[3] - G.fix[0], 0);
+        const double Pl = Pvs[G.pass_fix[0]], Ps0 = Pvs[G.pass_fix[2]], Pfg = Pvs[G.pass_fix[3]],
+                     Ps1 = Pvs[G.pass_fix[4]];
+        auto pfx = [&](double v) { return v == P.lower ? Pl : v == P.sg0 ? Ps0 : v == P.fg ? Pfg : Ps1; };
+        const double r0 = Pfg - Pl;
+        const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        bracket(r0, nl, nu, pfx(nu) - pfx(nl));
+        const int* Bl = Bls;
+        const int* Ch = Chs;
+        const double* Pv = Pvs;
+        int ilo = 0, ihi = 0;                              // boundary indices of the cell's ends
+        if (br == 0) { ilo = G.pass_fix[1]; ihi = G.pass_fix[2]; }
+        if (br == 1) { ilo = G.pass_fix[2]; ihi = G.pass_fix[3]; }
+        if (br == 3) { ilo = G.pass_fix[3]; ihi = G.pass_fix[4]; }
+        if (br == 2) {                                     // pass B over the bracket's cell (sg1, vmax]
+            Bl = Bls + G.pass_ma;
+            Ch = Chs + G.pass_ma;
+            Pv = Pvs + G.pass_ma;
+            pass(plo, phi, Bl, Pvs + G.pass_ma, G.pass_mb);
+            nodes += phi - plo;
+            ilo = 0;
+            ihi = G.pass_mb - 1;
         }
-        // beyond the tabulated tree (ties pile up): one searched level at a time
-        while (it < P.K && phi - plo > TCAP) {
+        stamp(3);
+        // the pruned tree's levels from LDS, no barrier: slab = difference of two prefixes
+        int im = br >= 0 ? G.pass_root[br] : -1;
+        while (im >= 0 && it < P.K && phi - plo > TCAP) {
             const double mid = (lo + hi) / 2;
             if (tid == 0) sn[it] = mid;
             if (nt < 0 && !(hi - lo > P.tol)) nt = it;
-            const int pm = sorted_ub(G.vs, plo, phi, mid);
-            const double val = team_sum(ustack ? range_sum(plo, pm) : range_sum(pm, phi));
-            nodes += ustack ? pm - plo : phi - pm;
-            if (level(mid, val)) { lo = mid; plo = pm; }
-            else                 { hi = mid; phi = pm; }
+            const double Pm = Pv[im];
+            const int c = Ch[im];
+            if (level(mid, ustack ? Pm - Pv[ilo] : Pv[ihi] - Pm)) { lo = mid; plo = Bl[im]; ilo = im; im = (c >> 16) - 1; }
+            else                                                 { hi = mid; phi = Bl[im]; ihi = im; im = (c & 0xFFFF) - 1; }
+            h = 2 * h + (ustack ? 1 : 0);
             ++it;
         }
-    } else {
+      }
+    }
+    if (!passed) {
         const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));   // (lower, fg]
         stamp(2);
         nodes += max(G.fix[2] - G.fix[0], 0);
@@ -907,6 +805,9 @@ __global__ __launch_bounds__(NT, SWEEP ? CVQ_SWEEP_MIN_WAVES : sorted_min_waves(
         stamp(3);
         nodes += max(fixpos(nu) - fixpos(nl), 0);
         bracket(r0, nl, nu, nr);
+    }
+    // the remaining levels above the tail: one range sum + one workgroup reduction each
+    {
         int pmt = h < tsz ? tr[h] : 0;                     // ub(mid) of heap node h, loaded a level ahead
         for (; it < P.K && phi - plo > TCAP; ++it) {
             const double mid = (lo + hi) / 2;

@@ -28,8 +28,8 @@ struct SortedLaunch {
 
 template <int NT, int COP, bool MSM, int DIM, int PM, bool FUSED, int LAY>
 void sorted_launch_l(const SortedLaunch& L) {
-    if constexpr (DIM == 2 && NT == kSortNT) {
-        if (L.sweep && L.mode == 0) {                  // SWEEP: one pass per cell (2-D solves)
+    if constexpr (DIM == 2) {
+        if (L.sweep && L.mode == 0) {                  // SWEEP: passes for the first levels (2-D solves)
             hipLaunchKernelGGL((k_sorted<COP, MSM, DIM, NT, PM, FUSED, LAY, true>), dim3((unsigned)L.T),
                                dim3(NT), sorted_lds_bytes(L.S.n, NT, DIM, true, LAY), L.stream, L.S, L.P,
                                L.G, L.a, L.tA, L.tB, L.pi, L.mode, L.bounds, L.out, L.snaps, L.hdr, L.stamps);
@@ -44,9 +44,6 @@ void sorted_launch_l(const SortedLaunch& L) {
 template <int NT, int COP, bool MSM, int DIM, int PM, bool FUSED>
 void sorted_launch_f(const SortedLaunch& L) {
     if constexpr (DIM == 2) {
-        if constexpr (COP == CVQ_STUDENT && PM > 0 && NT == kSortNT) {     // kLay2W: SWEEP's folded records
-            if (L.G.layout == kLay2W) { sorted_launch_l<NT, COP, MSM, DIM, PM, FUSED, kLay2W>(L); return; }
-        }
         sorted_launch_l<NT, COP, MSM, DIM, PM, FUSED, kLay2>(L);
     } else {
         if (sorted_layout(DIM, L.S.n) == kLay3F) sorted_launch_l<NT, COP, MSM, DIM, PM, FUSED, kLay3F>(L);
