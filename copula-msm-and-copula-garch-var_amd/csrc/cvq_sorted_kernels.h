@@ -46,8 +46,19 @@ namespace cvq {
 __host__ __device__ constexpr int sorted_tail_per_lane(int dim) { return dim == 2 ? CVQ_SORT_TAIL2 : CVQ_SORT_TAIL3; }
 __host__ __device__ constexpr int sorted_tail_cap(int dim) { return 64 * sorted_tail_per_lane(dim); }
 constexpr int kSortMaxDepth = 16;                     // deepest tabulated bisection level
+// Block tail (exact dyadic walks, after the first bisection level): once the cell holds at most
+// NT * kSortBlk nodes the whole workgroup evaluates it once in v* order, kSortBlk consecutive
+// positions per thread, and one block scan + two crossing searches decide every remaining level
+// (COMPACT's block tail) -- instead of one range sum + one workgroup reduction per level.
+#ifndef CVQ_SORT_BLK
+#define CVQ_SORT_BLK 8
+#endif
+constexpr int kSortBlk = CVQ_SORT_BLK;
 #ifndef CVQ_SORT_ILP
 #define CVQ_SORT_ILP 4
+#endif
+#ifndef CVQ_SORT_SKIP
+#define CVQ_SORT_SKIP 1            // range sums skip the partial rounds' slots past the range
 #endif
 // zero words after the node lists: a range sum's prefetch reads up to one round (kSortIlp x the
 // widest workgroup) past its range
@@ -552,8 +563,12 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
                 ip += ILP * NT;
 #pragma unroll
                 for (int u = 0; u < ILP; ++u) cn[u] = ip[u * NT];
+                // a slot whose wave starts at or past p1 holds no node of the range (short ranges):
+                // skipped (the test is wave-uniform, lane 0 holds the wave's lowest position)
+                const int wb = __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
                 for (int u = 0; u < ILP; ++u) {
+                    if (CVQ_SORT_SKIP && wb + u * NT >= p1) continue;
                     const int q = p + u * NT;
                     const double v = node_fast(c[u]);
                     acc[u] += (q >= p0 && q < p1) ? v : 0.0;
@@ -585,8 +600,10 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
                 p += ILP * NT;
             }
             if (p < p1) {                                  // last round: positions from p1 on masked
+                const int wb = __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
                 for (int u = 0; u < ILP; ++u) {
+                    if (CVQ_SORT_SKIP && wb + u * NT >= p1) continue;
                     const double v = node_fast(cn[u]);
                     acc[u] += p + u * NT < p1 ? v : 0.0;
                 }
@@ -806,10 +823,12 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         nodes += max(fixpos(nu) - fixpos(nl), 0);
         bracket(r0, nl, nu, nr);
     }
-    // the remaining levels above the tail: one range sum + one workgroup reduction each
+    // the remaining levels above the tails: one range sum + one workgroup reduction each
+    const bool blk = P.exact_walk != 0;                    // block tail usable (after one level)
+    constexpr int BCAP = NT * kSortBlk;
     {
         int pmt = h < tsz ? tr[h] : 0;                     // ub(mid) of heap node h, loaded a level ahead
-        for (; it < P.K && phi - plo > TCAP; ++it) {
+        while (it < P.K && phi - plo > TCAP && !(blk && it >= 1 && phi - plo <= BCAP)) {
             const double mid = (lo + hi) / 2;
             if (tid == 0) sn[it] = mid;
             if (nt < 0 && !(hi - lo > P.tol)) nt = it;
@@ -825,11 +844,97 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
             if (tab) h = 2 * h + (ustack ? 1 : 0);         // children: (lo, mid) = 2h, (mid, hi) = 2h + 1
             pmt = ustack ? pr : pl;
             if (it < 15) stamp(5 + it);
+            ++it;
         }
     }
 
+    // ---- block tail: the cell (lo, hi] = v*-sorted positions [plo, phi), TCAP < phi - plo <= BCAP.
+    // Thread tid evaluates positions plo + tid * kSortBlk + m in order; a block scan turns the
+    // values into F at every node threshold (F = prev + prefix when the last level moved lo, else
+    // prev - (cell total - prefix): the reference's adjust_integral chain after its first level).
+    // F is non-decreasing in v (node values >= 0; a NaN makes every later F NaN), so every
+    // remaining decision "F(mid) < obj" is "mid < v_c", v_c the first tie-group end where
+    // !(F < obj), and the zeros of F one interval (zero_interval): dyadic_walk writes them all.
+    const bool blk_tail = it < P.K && blk && it >= 1 && phi - plo > TCAP;   // workgroup-uniform
+    if (blk_tail) {
+        constexpr int KB = kSortBlk;
+        const int cnt = phi - plo;
+        const int e0 = tid * KB;                           // my first cell entry
+        uint32_t wd[KB];
+        double vv[KB + 1];                                 // v* of my entries and of the next one
+#pragma unroll
+        for (int m = 0; m < KB; ++m) wd[m] = e0 + m < cnt ? G.tidx[plo + e0 + m] : 0u;
+#pragma unroll
+        for (int m = 0; m <= KB; ++m) vv[m] = e0 + m < cnt ? G.tvs[plo + e0 + m] : __builtin_inf();
+        double pre[KB];                                    // my inclusive prefix
+        double run = 0.0;
+        auto eval_cell = [&](auto nodef) {
+#pragma unroll
+            for (int m = 0; m < KB; ++m) {
+                const double v = e0 + m < cnt ? nodef(wd[m]) : 0.0;
+                run += v;
+                pre[m] = run;
+            }
+        };
+        if (fast) eval_cell(node_fast);
+        else eval_cell(node_generic);
+        nodes += cnt;
+        // block exclusive scan of the thread totals (one barrier); the tail buffer is free here
+        double* wt = (double*)tail;                        // [NT / 64] wave totals
+        int* ew = (int*)(wt + NT / 64);                    // [NT / 64][4] first crossing / zero / positive
+        const double incl = wave_incl_scan_f64(run);
+        if (lane == 63) wt[tid >> 6] = incl;
+        __syncthreads();
+        double base = incl - run, Stot = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) {
+            const double x = wt[w];
+            base += (w < (tid >> 6)) ? x : 0.0;
+            Stot += x;
+        }
+        const double Flo = ustack ? prev : prev - Stot;   // F just above lo
+        int mc = KB, ma = KB, mz = KB;
+#pragma unroll
+        for (int m = KB - 1; m >= 0; --m) {
+            if (!(e0 + m < cnt && vv[m + 1] > vv[m])) continue;   // tie-group ends only (inf past the cell)
+            const double pa = base + pre[m];
+            const double Fv = ustack ? prev + pa : prev - (Stot - pa);
+            if (!(Fv < P.obj)) mc = m;
+            if (Fv == 0.0) ma = m;
+            if (!(Fv <= 0.0)) mz = m;
+        }
+        const unsigned long long bc = __ballot(mc < KB), ba = __ballot(ma < KB), bz = __ballot(mz < KB);
+        const int lc = bc ? (int)__builtin_ctzll(bc) : 0, la = ba ? (int)__builtin_ctzll(ba) : 0,
+                  lz = bz ? (int)__builtin_ctzll(bz) : 0;
+        const int mcl = __shfl(mc, lc, 64), mal = __shfl(ma, la, 64), mzl = __shfl(mz, lz, 64);
+        if (lane == 0) {
+            int* e = ew + 4 * (tid >> 6);
+            e[0] = bc ? ((tid >> 6) * 64 + lc) * KB + mcl : kNoPos;
+            e[1] = ba ? ((tid >> 6) * 64 + la) * KB + mal : kNoPos;
+            e[2] = bz ? ((tid >> 6) * 64 + lz) * KB + mzl : kNoPos;
+        }
+        __syncthreads();
+        stamp(29);
+        if (tid < 64) {
+            int ec = kNoPos, ea = kNoPos, ez = kNoPos;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) {                   // waves in position order: first wins
+                const int* e = ew + 4 * w;
+                if (ec == kNoPos && e[0] != kNoPos) ec = e[0];
+                if (ea == kNoPos && e[1] != kNoPos) ea = e[1];
+                if (ez == kNoPos && e[2] != kNoPos) ez = e[2];
+            }
+            const int kc = !(Flo < P.obj) ? 0 : (ec == kNoPos ? 1 : 2);
+            const double vcs = kc == 2 ? G.tvs[plo + ec] : 0.0;
+            const double inf = __builtin_inf();
+            double vza, vzb;
+            zero_interval(Flo, (Flo < 0.0 && ea != kNoPos) ? G.tvs[plo + ea] : inf,
+                          (!(Flo > 0.0) && ez != kNoPos) ? G.tvs[plo + ez] : inf, vza, vzb);
+            dyadic_walk(P, kc, vcs, vza, vzb, lo, hi, it, nt, mask, sn);
+        }
+    }
     // ---- tail: the bracket's <= TCAP nodes -> LDS, wave 0 finishes the levels
-    if (it < P.K) {
+    if (!blk_tail && it < P.K) {
         const int tot = phi - plo;
         // exact walk: the cell's nodes in v* order (same node set: plo, phi are segment boundaries)
         const uint32_t* tix = P.exact_walk ? G.tidx : G.idx;
