@@ -27,6 +27,8 @@ for _ in range(3):
 buf = np.zeros(T * 32, dtype=np.uint64)
 N.check(N.lib().cvq_plan_debug_stamps(p._h, N.ptr(buf), buf.size), "stamps")
 st = buf.reshape(T, 32).astype(np.int64)
+if "--dump" in sys.argv:                       # raw per-date stamps + VaR for offline analysis
+    np.savez_compressed(sys.argv[sys.argv.index("--dump") + 1], st=st, var=var, ptf=ptf)
 if STRAT in ("compact", "sorted") and (st[:, 27] != 0).any():
     # placement: HW_ID bits cu 11:8, sh 12, se 15:13; XCC_ID low bits in the high word
     hw = st[:, 27] & 0xFFFFFFFF
