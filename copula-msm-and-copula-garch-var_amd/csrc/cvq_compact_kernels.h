@@ -603,11 +603,16 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             wr = S.F[i];
             wc = S.F[(size_t)n + i];
         }
-        if (!isfinite(A[0]) || !isfinite(B[0]) || !isfinite(A[1]) || !isfinite(B[1])) bad |= 1;
-        col[kColRec * i] = A[1];
-        col[kColRec * i + 1] = B[1] * wc;
+        // GARCH / UKF Student: a dead entry (z = +-inf or NaN: u in {0, 1}) zeroes its nodes in the
+        // reference (k_sorted's table phase, student.py:130-131, :166-167, nan_to_num): record
+        // (0, scale 0) on the fast path rather than deferring the date to the generic kernel
+        const bool d0 = COP == CVQ_STUDENT && !MSM && !isfinite(A[0]);
+        const bool d1 = COP == CVQ_STUDENT && !MSM && !isfinite(A[1]);
+        if ((!d0 && (!isfinite(A[0]) || !isfinite(B[0]))) || (!d1 && (!isfinite(A[1]) || !isfinite(B[1])))) bad |= 1;
+        col[kColRec * i] = d1 ? 0.0 : A[1];
+        col[kColRec * i + 1] = d1 ? 0.0 : B[1] * wc;
         double* rr = rowr + RR * i;
-        fast_row_consts<COP, SI>(S, A[0], B[0], wr, rr);
+        fast_row_consts<COP, SI>(S, d0 ? 0.0 : A[0], d0 ? 0.0 : B[0], wr, rr);
         if constexpr (GEN) {
             colg[cgs * i] = B[1];                                  // may share rr[2..3] (Student / Gaussian)
             colg[cgs * i + 1] = wc;

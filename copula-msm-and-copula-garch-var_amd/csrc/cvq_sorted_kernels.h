@@ -346,9 +346,11 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
             } else {
                 w = S.F[(size_t)ax * n + i];
             }
-            if (!isfinite(A) || !isfinite(B)) bad |= 1;
-            if (!(B * w > 0.0)) bad |= 1;                  // fast records take logs of B w
-            if (!(fabs(A) < 1.0e15)) bad |= 1;             // fast powers / exps need a bounded quadratic form
+            if (!(COP == CVQ_STUDENT && !MSM && !isfinite(A))) {   // dead entries: below
+                if (!isfinite(A) || !isfinite(B)) bad |= 1;
+                if (!(B * w > 0.0)) bad |= 1;              // fast records take logs of B w
+                if (!(fabs(A) < 1.0e15)) bad |= 1;         // fast powers / exps need a bounded quadratic form
+            }
             eA[k][ax] = A;
             eB[k][ax] = B;
             eW[k][ax] = w;
@@ -427,13 +429,21 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
             r[0] = ax == 0 ? -2.0 * z : (S.theta - 1.0) * z;
             r[1] = (ax == 0 ? S.theta : 1.0) * (B * w);
         } else {                                           // Student: z and scale
-            const double sc = (ax == 0 ? S.term1 : 1.0) * B * (ax == 0 && DIM == 3 ? arest : w);
+            // GARCH / UKF: a dead entry (u in {0, 1}: z = +-inf, or NaN) zeroes every node through
+            // it in the reference -- a non-finite z gives multivariate and univariate t pdfs of
+            // 0 (student.py:130-131, :166-167), 0 / 0 = NaN, nan_to_num -> 0
+            // (garch_integration_function.py:48) -- so its record is (0, 0): those nodes evaluate
+            // to +0 on the fast path (scale 0 times a finite power) instead of sending the date to
+            // the generic path (27% of cfg 5's dates hold such grid-edge entries)
+            const bool dead = !MSM && !isfinite(z);
+            const double sc = dead ? 0.0 : (ax == 0 ? S.term1 : 1.0) * B * (ax == 0 && DIM == 3 ? arest : w);
+            const double zr = dead ? 0.0 : z;
             double* r = ax == 0 ? fr0 + 2 * i : ax == DIM - 1 ? fr2 + 2 * i : fr1 + R1 * i;
-            r[0] = z;
+            r[0] = zr;
             r[1] = sc;
             if (DIM == 3 && ax == 0) {                                       // plane i1 == 0 (Q6)
-                fr0[2 * (n + i)] = z;
-                fr0[2 * (n + i) + 1] = S.term1 * B * w;
+                fr0[2 * (n + i)] = zr;
+                fr0[2 * (n + i) + 1] = dead ? 0.0 : S.term1 * B * w;
             }
         }
       }
