@@ -77,7 +77,7 @@ def parse():
                     help="total dates split over the ranks (strong scaling); default: --dates-per-gpu per rank")
     ap.add_argument("--single", type=int, default=1, help="also time the one-batch-at-a-time solve (single_solve)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "prefix", "direct", "compact", "sorted", "sweep"],
-                    help="auto: COMPACT for 2-asset MSM, SORTED otherwise (engine.auto_strategy)")
+                    help="auto: COMPACT for 2-asset MSM and integer-power Student, SORTED otherwise (engine.auto_strategy)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the joblib CPU path (rank 0, N=1)")
     ap.add_argument("--cpu-dates", type=int, default=0,
                     help="CPU sample size (0 = four per worker: ~15 s of joblib work on config 2)")
@@ -174,6 +174,8 @@ def main():
     args = engine.solve_args(ptf_mean)
     fast_ok = c.model == "msm" and bool(np.array_equal(                # the kernel's own rank-1 test, on the host
         ipt[1], (ipt[0][:, 0, :, None] * ipt[0][:, 1, None, :]).reshape(ipt[1].shape))) if c.dim == 2 else False
+    if c.model != "msm" and c.dim == 2 and c.copula == "student":   # cvq_plan.hip fast_path_proven's Student rule
+        fast_ok = bool(np.all(np.isfinite(ipt[0]) & (ipt[0] > 0.0)))
     # `inflight` batches in flight: plan i (its own HIP stream, scratch, output and, when
     # sharded, its own process group) solves steps i, i + inflight, ...  Consecutive
     # batches are independent, so the next one fills the CUs the current one's last
@@ -437,7 +439,9 @@ def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):
         k = i % nf
         with torch.cuda.stream(streams[k]):
             mts[k].run(r_dev, streams[k].cuda_stream)
-            plans[k].set_dates_device(per, *ptrs(mts[k]), fast=c.model == "msm")   # cvq_msm_tables: rank-1 pi
+            # cvq_msm_tables: rank-1 pi; GARCH / UKF Student: any finite sigma > 0 (a failed forecast
+            # window is reported by the forecast stage, a violating date fails the solve loudly)
+            plans[k].set_dates_device(per, *ptrs(mts[k]), fast=c.model == "msm" or (c.dim == 2 and c.copula == "student"))
             plans[k].solve_device(args, vars_[k].data_ptr())
 
     for i in range(a.warmup):

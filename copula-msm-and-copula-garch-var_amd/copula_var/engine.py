@@ -48,8 +48,10 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None, copula: Optiona
                   copula_params=None) -> str:
     """The measured-fastest strategy per workload (cfg 1-5 on one MI355X)
     among those that run it: COMPACT for 2-asset MSM (cfg 2: 20.3M vs SORTED 16.4M
-    VaR-dates/s), SORTED for 2-asset GARCH / UKF (cfg 1, 3, 5: 1.2-1.4x COMPACT) and for
-    3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
+    VaR-dates/s) and for 2-asset GARCH / UKF with an integer-power Student copula (cfg 5:
+    25.2M vs 22.5M since r05's grid-edge fast records), SORTED for the other 2-asset
+    GARCH / UKF copulas (cfg 3 Plackett: 8.1M vs 6.3M; cfg 1 Gaussian: 33.8M vs 26.9M) and
+    for 3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
     bounds the choice: every 2-D strategy takes n <= 512 (the plan's limit, so a 2-D
     rule never picks a strategy that fails later), 3-D SORTED n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
     takes n > 255.  SORTED and PREFIX hold the nodes with level <= v_cap only;
@@ -60,7 +62,9 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None, copula: Optiona
             raise ValueError(f"num_points <= {MAX_N} (every strategy: cvq_plan_create), got {n}")
         # a fitted (non-integer) Student nu: SORTED (cfg 2 at nu = 5.364: 9.4M vs COMPACT 7.8M
         # VaR-dates/s; COMPACT's general-power instance needs 104 VGPRs, 4 waves per SIMD)
-        return "compact" if model == "msm" and not general_power(copula, copula_params) else "sorted"
+        if general_power(copula, copula_params):
+            return "sorted"
+        return "compact" if model == "msm" or copula == "student" else "sorted"
     if n is None or n <= SORTED_MAX_N[3]:
         return "sorted"
     raise ValueError(f"3-asset grids support num_points <= {SORTED_MAX_N[3]} (SORTED), got {n}")

@@ -1488,12 +1488,65 @@ __device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const 
     return true;
 }
 
+// Forecast-only UKF pass (k_ukf_forecast, k_ukf_sigma): ukf_pass's recursion with the step's
+// dependent chain shortened -- w / exp(X) as w * exp(-X), the three (.) / Z and (h / Z) of the
+// update as one reciprocal of Z (v_rcp_f64 + two Newton steps, ~1 ulp) times the sums, no
+// log-likelihood -- so a step waits on one reciprocal instead of two IEEE division stages
+// (one window per thread, ~150 waves on the chip: the forecast is latency-bound).  A few ulp
+// per step; the filter contracts, and sigma stays within 1e-12 of the reference's goldens
+// (tests/test_gpu_parity.py).  Same failure rule as ukf_pass (estimate.py:219-220, :270-271).
+__device__ bool ukf_forecast_pass(const UkfConst& C, double a, double l, double q, const double* w, long long N,
+                                  double* xmean_last) {
+    double x = l, var = q;
+    double xm = 0.0;
+    for (long long t = 0; t < N; ++t) {
+        const double dvar = (var <= 0) ? var + 1e-8 : var;
+        const double c0 = sqrt(dvar);
+        const double X1a[5] = {x, x + C.phi * c0, x + C.phi * 0.0, x - C.phi * c0, x - C.phi * 0.0};
+        const double X1b[5] = {0.0, 0.0 + C.phi * 0.0, 0.0 + C.phi * 1.0, 0.0 - C.phi * 0.0, 0.0 - C.phi * 1.0};
+        double X[5];
+        for (int i = 0; i < 5; ++i) X[i] = a * (X1a[i] - l) + l + q * X1b[i];
+        xm = X[0] * C.wm0;
+        for (int i = 1; i < 5; ++i) xm += X[i] * C.wm1;
+        double P = 0.0;
+        for (int i = 0; i < 5; ++i) {
+            const double d = X[i] - xm;
+            P += (d * (i == 0 ? C.wc0 : C.wc1)) * d;
+        }
+        const double sP = sqrt(P);
+        const double X2[3] = {xm, xm + C.phi * sP, xm - C.phi * sP};
+        const double wt = w[t];
+        double h[3], Z = 0.0, S1 = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double eta = wt * exp(-X2[i]);
+            h[i] = (kInvSqrt2Pi * exp(-0.5 * (eta * eta))) * fabs(eta);
+            const double wi = (i == 0 ? C.wm2_0 : C.wm2_1) * h[i];
+            Z += wi;
+            S1 += wi * X2[i];
+        }
+        if (Z <= 0 || Z < 1e-10) return false;
+        const double rz = fast_rcp(Z);
+        const double mean = S1 * rz;
+        double S2 = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double d = X2[i] - mean;
+            S2 += ((i == 0 ? C.wm2_0 : C.wm2_1) * h[i]) * (d * d);
+        }
+        const double v2 = S2 * rz;
+        if (isnan(mean) || isnan(v2) || isnan(Z)) return false;
+        x = mean;
+        var = v2;
+    }
+    *xmean_last = xm;
+    return true;
+}
+
 __global__ void k_ukf_forecast(UkfConst C, double a, double l, double q, const double* __restrict__ r, long long n_in,
                                long long T, double* __restrict__ out, int* err) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    double xm, ll;
-    if (!ukf_pass(C, a, l, q, r + t, n_in, &xm, &ll)) {
+    double xm;
+    if (!ukf_forecast_pass(C, a, l, q, r + t, n_in, &xm)) {
         atomicOr(err, 1);
         out[t] = __builtin_nan("");
         return;
@@ -1512,8 +1565,8 @@ __global__ void k_ukf_sigma(UkfConst C, UkfPrmN U, const double* __restrict__ r,
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const int d = blockIdx.y;
-    double xm, ll;
-    if (!ukf_pass(C, U.a[d], U.l[d], U.q[d], r + d * rstride + t, n_in, &xm, &ll)) {
+    double xm;
+    if (!ukf_forecast_pass(C, U.a[d], U.l[d], U.q[d], r + d * rstride + t, n_in, &xm)) {
         atomicOr(err, 1);
         out[t * gridDim.y + d] = __builtin_nan("");
         return;

@@ -783,6 +783,15 @@ bool fast_path_proven(const StaticDev& S, const std::vector<double>& hx, long lo
         return true;
     }
     if (S.copula == CVQ_STUDENT && !(S.nu >= 1.0)) return false;
+    if (S.copula == CVQ_STUDENT) {
+        // Student (r05): an entry with u in {0, 1} is a dead record on the fast path (its nodes
+        // are 0 in the reference, cvq_compact_kernels.h table phase), and a u strictly inside
+        // is >= 2^-54 (1 + erf rounds to 0 or >= 2^-53), whose quantile at nu >= 1 is finite
+        // (|z| <= ~6e15) with a finite density ratio: any finite sigma > 0 takes the fast path
+        for (long long e = 0; e < 2 * T; ++e)
+            if (!(std::isfinite(a[e]) && a[e] > 0.0)) return false;
+        return true;
+    }
     double xmax = 0.0;
     for (double x : hx) xmax = std::max(xmax, std::fabs(x));
     for (long long e = 0; e < 2 * T; ++e)

@@ -39,7 +39,7 @@ def _dates(z, sl=slice(None)):
     return [z["sigma_forecasts"][sl]]
 
 
-@pytest.mark.parametrize("cfg,strategy", [(2, "auto"), (5, "auto"), (5, "compact"), (3, "auto")])
+@pytest.mark.parametrize("cfg,strategy", [(2, "auto"), (5, "auto"), (5, "sorted"), (3, "auto")])
 def test_full_batch_heavy_first_matches_oracle(cfg, strategy):
     z = dict(np.load(os.path.join(GOLDEN, f"fullbatch_cfg{cfg}.npz"), allow_pickle=False))
     p = _plan(z, strategy, True)

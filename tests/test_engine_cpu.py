@@ -21,6 +21,11 @@ def test_auto_strategy_rules():
     assert auto_strategy("msm", 2, 256, "student", [5.0, 0.5]) == "compact"   # nu + 2 integer: no log / exp
     assert auto_strategy("msm", 2, 256, "student", [4.5, 0.5]) == "sorted"
     assert auto_strategy("msm", 2, 256, "gaussian", [0.5]) == "compact"
+    # GARCH / UKF: COMPACT for an integer-power Student copula (cfg 5), SORTED otherwise
+    assert auto_strategy("mean_reverting", 2, 256, "student", [6.0, 0.5]) == "compact"
+    assert auto_strategy("garch", 2, 256, "student", [5.364, 0.5]) == "sorted"
+    assert auto_strategy("garch", 2, 512, "plackett", [3.0]) == "sorted"
+    assert auto_strategy("garch", 2, 64, "gaussian", [0.6]) == "sorted"
     with pytest.raises(ValueError):
         auto_strategy("msm", 3, 256)                        # no 3-D strategy takes n > 255
 

@@ -8,7 +8,7 @@ stage; tests/golden/gen_fullbatch.py).  Here the HIP solve of the same full batc
 give the same VaR vector bit for bit and the same global iteration count -- on one plan,
 and split into 2 and 4 contiguous date blocks (plans) joined by the packed finalize
 (cvq_solve_finalize_packed, the single all-gather's layout).  The strategy
-is auto (COMPACT for cfg 2, SORTED for cfg 3 / 5); cfg 5 also runs COMPACT."""
+is auto (COMPACT for cfg 2 / 5, SORTED for cfg 3); cfg 5 also runs SORTED."""
 import os
 
 import numpy as np
@@ -19,7 +19,7 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-CASES = [(2, "auto"), (5, "auto"), (5, "compact"), (3, "auto")]
+CASES = [(2, "auto"), (5, "auto"), (5, "sorted"), (3, "auto")]
 
 
 @pytest.fixture(scope="module", autouse=True)

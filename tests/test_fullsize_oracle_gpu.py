@@ -9,7 +9,7 @@ taken from each BASELINE workload at its full grid size:
 
 * cfg 2 (MSM Student, n = 256): 8 dates of the 1000-date workload, COMPACT (auto);
 * cfg 3 (GARCH Plackett, n = 512): 4 dates of the 5000-date workload, SORTED (auto);
-* cfg 5 (UKF Student, n = 256): 4 dates of the 5000-date workload, SORTED (auto);
+* cfg 5 (UKF Student, n = 256): 4 dates of the 5000-date workload, COMPACT (auto);
 * cfg 1 (GARCH Gaussian, n = 64): all 50 dates.
 
 The dates are spread over the VaR range of the full batch (so every bracket class
@@ -96,9 +96,10 @@ def test_full_size_dates_match_oracle(cfg, T, S):
     assert np.array_equal(var, ref), (cfg, float(np.max(np.abs(var - ref))))
 
 
-@pytest.mark.parametrize("case", ["cfg1", "cfg5_n64", "cfg4_k4_n16"])
+@pytest.mark.parametrize("case", ["cfg1", "ukf_plackett_n64", "cfg4_k4_n16"])
 def test_auto_routes_levels_above_v_cap(case):
-    """auto = SORTED for 2-D GARCH / UKF and for 3-D; SORTED holds nodes up to v_cap = 0:
+    """auto = SORTED for 2-D GARCH / UKF with a Gaussian or Plackett copula and for 3-D;
+    SORTED holds nodes up to v_cap = 0:
     slabs and a solve that reach above 0 go to an unrestricted sibling (COMPACT in 2-D,
     SORTED with v_cap at the grid's top in 3-D) and still match the oracle."""
     from conftest import load_golden
@@ -168,6 +169,39 @@ def test_fast_path_proof_boundary_sigma_xmax_over_6_nu1():
     try:
         p.set_dates([sig])
         var, it = p.calc_var(0.0)
+    finally:
+        p.close()
+    assert it == ref_it
+    assert np.array_equal(var, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("nu", [1.0, 6.0])
+@pytest.mark.parametrize("strategy", ["compact", "sorted"])
+def test_fast_path_dead_entries_small_sigma(strategy, nu):
+    """GARCH / UKF Student dates whose grid reaches |x| / sigma ~ 70 (u = 0 or 1 at the grid
+    edges: z = +-inf, the reference zeroes those nodes) and ~ 8 (u down to ~1e-16: the
+    largest finite quantiles) take the fast path with dead records (r05; cfg 5 has such
+    dates): VaR bit-identical to the oracle, with the host's fast-path proof (COMPACT skips
+    its generic kernel) and in SORTED's per-date check."""
+    from conftest import load_golden
+    from copula_var.engine import QuadraturePlan
+    from oracle.quadrature import Problem, calc_var
+    z = load_golden("garch_student_n64")
+    x = z["x_values"]
+    sig = np.array(z["sigma_forecasts"], dtype=np.float64)
+    xmax = float(np.max(np.abs(x)))
+    sig[0::3] = xmax / 70.0
+    sig[1::3, 0] = xmax / 8.0
+    cp = np.array([nu, 0.5])
+    args = ("garch", "student", 2, x, z["step"], z["densities"], z["combos"], z["weights"], cp)
+    P = Problem(*args, sig)
+    ref, ref_it, _ = calc_var(P.compute_integral, P.T, 0.0)
+    p = QuadraturePlan(*args, strategy=strategy)
+    try:
+        p.set_dates([sig])
+        var, it = p.calc_var(0.0)
+        b = np.tile([-3.0, -2.0], (P.T, 1))
+        np.testing.assert_allclose(p.compute_integral(b), P.compute_integral(b), rtol=SLAB_RTOL, atol=SLAB_ATOL)
     finally:
         p.close()
     assert it == ref_it

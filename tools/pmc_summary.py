@@ -18,7 +18,7 @@ for i, a in enumerate(args):
     if a == "--dates-per-gpu": dates = int(args[i + 1])
     if a == "--strategy": strategy = args[i + 1]
 if strategy in (None, "auto"):                       # bench.py's auto: COMPACT for 2 assets, SORTED for 3
-    strategy = "compact" if cfg == 2 else "sorted"   # engine.auto_strategy for configs 1-5
+    strategy = "compact" if cfg in (2, 5) else "sorted"   # engine.auto_strategy for configs 1-5
 dates = {1: 50, 2: 1000, 3: 5000, 4: 2000, 5: 5000}.get(cfg, dates)
 for i, a in enumerate(args):
     if a == "--dates-per-gpu": dates = int(args[i + 1])
