@@ -81,7 +81,6 @@ def _declare(lib: C.CDLL) -> None:
         "cvq_plan_nodes_evaluated": (i32, [v, C.POINTER(i64)]),
         "cvq_set_dates": (i32, [v, i64, v, v, i32]),
         "cvq_set_fast_hint": (i32, [v, i32]),
-        "cvq_plan_set_dispatch_order": (i32, [v, i32]),
         "cvq_slab": (i32, [v, v, v, i32]),
         "cvq_solve": (i32, [v, C.POINTER(CvqSolveArgs), v, _ip, i32]),
         "cvq_snap_stride": (i32, [C.POINTER(CvqSolveArgs), _ip]),

@@ -107,7 +107,6 @@ class QuadraturePlan:
         self._wide: Optional["QuadraturePlan"] = None       # unrestricted sibling (auto, level > v_cap)
         self._dates = None                                  # last set_dates / set_dates_device arguments
         self._stream, self._timing, self._counting = None, False, False   # forwarded to the sibling
-        self._order: Optional[bool] = None
         self._last: Optional["QuadraturePlan"] = None       # plan of the last device solve (solve_status)
         if strategy == "auto":
             strategy = auto_strategy(model, self.dim, self._x.size, copula, self._cp)
@@ -156,8 +155,6 @@ class QuadraturePlan:
                 self._wide = QuadraturePlan(model, copula, dim, x, step, dens, combos, w, cp, vol_states=vs,
                                             v_cap=max(grid_top, float(top)), device=dev, strategy="sorted")
             self._wide.set_stream(self._stream)
-            if self._order is not None:
-                self._wide.set_dispatch_order(self._order)
             if self._dates is not None:
                 kind, args = self._dates
                 (self._wide.set_dates if kind == "host" else self._wide.set_dates_device)(*args)
@@ -183,15 +180,6 @@ class QuadraturePlan:
         self._stream = stream_handle
         if self._wide is not None:
             self._wide.set_stream(stream_handle)
-
-    def set_dispatch_order(self, heavy_first: bool) -> None:
-        """Workgroup order of the COMPACT / SORTED solves from the next set_dates on:
-        heavy-bracket dates first (cvq_plan_set_dispatch_order mode 1) or index order.
-        Results are unchanged bit for bit; only the schedule differs."""
-        N.check(N.lib().cvq_plan_set_dispatch_order(self._h, 1 if heavy_first else 0), "cvq_plan_set_dispatch_order")
-        self._order = bool(heavy_first)
-        if self._wide is not None:
-            self._wide.set_dispatch_order(heavy_first)
 
     KERNELS = {"tables": 0, "mass": 1, "solve": 2, "finalize": 3, "slab": 4}
 

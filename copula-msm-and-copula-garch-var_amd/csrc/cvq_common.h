@@ -59,7 +59,6 @@ struct SolveConst {
     int* fin_err;                 // [4]: error, kstop, N, workgroup ticket (0 between launches)
     int exact_walk;               // every bracket's bisection points are exact dyadics (dyadic_walk_ok):
                                   // COMPACT's tail walks its remaining levels in closed form, one per lane
-    const int* order;             // [T] date of each workgroup (dispatch order, cvq_set_dates); nullptr: identity
 };
 
 struct alignas(16) Header {       // per-rank solve summary, all-gathered across ranks
@@ -71,7 +70,7 @@ struct alignas(16) Header {       // per-rank solve summary, all-gathered across
 // Layout key of the structs passed between translation units (cvq_plan.hip launches the
 // kernels compiled in cvq_compact.hip / cvq_sorted.hip): a stale object fails its launch
 // with CVQ_ERR_STATE instead of reading misplaced pointers.
-constexpr size_t kAbiVersion = 5;
+constexpr size_t kAbiVersion = 6;
 __host__ __device__ constexpr size_t kernel_abi_key() {
     return kAbiVersion * 1000003u + sizeof(StaticDev) * 4099u + sizeof(SolveConst) * 67u + sizeof(Header);
 }

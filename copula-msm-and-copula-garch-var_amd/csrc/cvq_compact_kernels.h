@@ -524,7 +524,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     stamp(0);
     if (stamps && tid == 0) {
         stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
-        stamps[30] = blockIdx.x;                         // dispatch position (cvq_plan_set_dispatch_order)
+        stamps[30] = blockIdx.x;                         // dispatch position (placement analysis)
         // placement: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of this workgroup's first wave
         stamps[27] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                      ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
@@ -1047,7 +1047,7 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
     __shared__ int last;
     if constexpr (!GEN) {
         compact_date<COP, MSM, NT, RPT, PM, FUSED, false>(S, P, G, a, tA, tB, pi, stamps_out, snaps, hdr, defer,
-                                                          P.order ? (long long)P.order[blockIdx.x] : (long long)blockIdx.x);
+                                                          (long long)blockIdx.x);
         if (!P.fin_var) return;
         if (tid == 0) {
             __threadfence();                             // release: this date's snapshots + header bits / deferral

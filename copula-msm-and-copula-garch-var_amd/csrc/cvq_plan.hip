@@ -112,10 +112,6 @@ int compact_tail_cap();                      // cvq_compact.hip: the block tail'
 
 using namespace cvq;
 
-// default dispatch order of new plans (cvq_plan_set_dispatch_order); CVQ_DATE_ORDER=0 / 1 in the
-// environment overrides it at plan creation (A/B runs)
-constexpr int kOrderDefault = 0;
-
 struct cvq_plan {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -173,10 +169,6 @@ struct cvq_plan {
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
-    int* d_order = nullptr;      // [T] dispatch order of the dates (k_date_order at cvq_set_dates)
-    long long capOrder = 0;
-    int order_mode = kOrderDefault;   // cvq_plan_set_dispatch_order: 1 = heavy dates first
-    bool order_on = false;       // the solves read d_order (COMPACT / SORTED; set by cvq_set_dates)
     // SORTED: reachable nodes sorted by v* (device: packed indices + v*; host: v*),
     // ub() of the fixed levels and the bisection trees for the cached solve arguments
     std::vector<double> hvs;
@@ -844,10 +836,8 @@ SortedGeom sorted_geom(const cvq_plan* p, bool solve) {
     return G;
 }
 
-int launch_solve(cvq_plan* p, const SolveConst& P0, double* snaps, Header* hdr) {
+int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
     TimedScope ts(p, TK_SOLVE);
-    SolveConst P = P0;
-    P.order = p->order_on ? p->d_order : nullptr;
     if (sorted_family(p)) {
         int rc = ensure_sorted_tree(p, P);
         if (rc) return rc;
@@ -1061,7 +1051,6 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.fin_var = nullptr;
     P.fin_err = nullptr;
     P.exact_walk = dyadic_walk_ok(a, K) ? 1 : 0;
-    P.order = nullptr;                             // launch_solve: the plan's dispatch order
     return P;
 }
 
@@ -1167,7 +1156,6 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     if (rc) return rc;
 
     cvq_plan* p = new cvq_plan();
-    if (const char* e = getenv("CVQ_DATE_ORDER")) p->order_mode = atoi(e) != 0 ? 1 : 0;
     p->device = device;
     p->strategy = s->strategy;
     p->v_cap = s->v_cap;
@@ -1357,7 +1345,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
                     (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_pass,
-                    (void*)p->d_pidx, (void*)p->d_pvs, (void*)p->d_order})
+                    (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
@@ -1459,14 +1447,6 @@ int32_t cvq_plan_nodes_evaluated(cvq_plan* p, int64_t* total) {
     return CVQ_OK;
 }
 
-int32_t cvq_plan_set_dispatch_order(cvq_plan* p, int32_t mode) {
-    CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
-    CVQ_REQUIRE(mode == 0 || mode == 1, CVQ_ERR_INVALID, "dispatch order mode must be 0 or 1");
-    p->order_mode = mode;
-    p->order_on = false;                           // takes effect at the next cvq_set_dates
-    return CVQ_OK;
-}
-
 int32_t cvq_set_fast_hint(cvq_plan* p, int32_t on) {
     CVQ_REQUIRE(p != nullptr, CVQ_ERR_INVALID, "plan is NULL");
     p->fast_hint = on != 0;
@@ -1507,17 +1487,6 @@ int32_t cvq_set_dates(cvq_plan* p, int64_t T, const double* a, const double* b, 
         p->in_pi = p->d_pi;
     }
     p->fast_hint = mem != CVQ_MEM_DEVICE && fast_path_proven(S, p->hx, T, a, b);
-    p->order_on = p->order_mode == 1 && (sorted_family(p) || p->strategy == CVQ_STRATEGY_COMPACT);
-    if (p->order_on) {                             // heavy dates first (k_date_order), on the plan's stream
-        if (p->capOrder < T) {
-            int rc = dev_alloc(&p->d_order, (size_t)T);
-            if (rc) return rc;
-            p->capOrder = T;
-        }
-        hipLaunchKernelGGL(k_date_order, dim3(1), dim3(kOrderNT), 0, p->stream, S, p->in_a, p->d_uvs, (long long)T,
-                           p->d_order);
-        CVQ_HIP_CHECK(hipGetLastError());
-    }
     if (S.model != CVQ_MSM && realloc) {          // GARCH/UKF: pi_t = [1.0] (Q = 1), set once
         std::vector<double> ones((size_t)p->capT * S.Q, 1.0);
         CVQ_HIP_CHECK(hipMemcpyAsync(p->d_pi, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice,

@@ -62,77 +62,6 @@ __global__ void k_phi(StaticDev S, const double* __restrict__ uvs, double* __res
     const double xs = S.x[i] / uvs[ds];
     phi[idx] = 0.5 * (1.0 + erf(xs / kInvSqrt2));
 }
-
-// ------------------------------------------------- dispatch order of a batch's dates
-// order[b] = the date the solve's workgroup b takes: ascending predicted portfolio scale
-// s_t = sum_d (w_d sigma_td)^2 (GARCH / UKF: sigma_td = a[t][d]; MSM: the state-averaged
-// scale sum_s f_tds sigma_ds).  A small scale puts the VaR in the (-2, 0] bracket, whose cell
-// holds ~2.5x the nodes of the others, so the heavy dates are
-// dispatched first and the last workgroups to start are light ones (longest-first).  Only
-// the schedule changes: every date's result is independent of the order.  One workgroup:
-// log-scale buckets (kOrderB) filled by LDS atomics, a block scan, a scatter.  A
-// non-finite scale goes to the last bucket; any input gives a permutation.
-constexpr int kOrderNT = 1024, kOrderB = 1024;
-__global__ __launch_bounds__(kOrderNT) void k_date_order(StaticDev S, const double* __restrict__ a,
-                                                         const double* __restrict__ uvs, long long T,
-                                                         int* __restrict__ order) {
-    __shared__ int cnt[kOrderB];
-    __shared__ float wlo[kOrderNT / 64], whi[kOrderNT / 64];
-    __shared__ int wsum[kOrderNT / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int q = S.model == CVQ_MSM ? S.q : 1;
-    auto lkey = [&](long long t) -> float {
-        double s = 0.0;
-        for (int d = 0; d < S.dim; ++d) {
-            double sg = 0.0;
-            const double* f = a + (t * S.dim + d) * q;
-            if (S.model == CVQ_MSM) {
-                for (int k = 0; k < q; ++k) sg = fma(f[k], uvs[d * q + k], sg);
-            } else {
-                sg = f[0];
-            }
-            const double w = d == 0 ? S.w0 : d == 1 ? S.w1 : S.w2;
-            s = fma(w * sg, w * sg, s);
-        }
-        return __logf((float)s);
-    };
-    for (int b = tid; b < kOrderB; b += kOrderNT) cnt[b] = 0;
-    float lo = __builtin_inff(), hi = -__builtin_inff();
-    for (long long t = tid; t < T; t += kOrderNT) {
-        const float k = lkey(t);
-        if (__builtin_isfinite(k)) { lo = fminf(lo, k); hi = fmaxf(hi, k); }
-    }
-    for (int o = 32; o; o >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, o, 64));
-        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
-    }
-    if (lane == 0) { wlo[wv] = lo; whi[wv] = hi; }
-    __syncthreads();
-    lo = wlo[0];
-    hi = whi[0];
-    for (int w = 1; w < kOrderNT / 64; ++w) { lo = fminf(lo, wlo[w]); hi = fmaxf(hi, whi[w]); }
-    const float sc = hi > lo ? (float)(kOrderB - 1) / (hi - lo) : 0.0f;
-    auto bucket = [&](long long t) -> int {
-        const float x = (lkey(t) - lo) * sc;
-        return x >= 0.0f ? min((int)x, kOrderB - 1) : (x < 0.0f ? 0 : kOrderB - 1);   // NaN: last
-    };
-    for (long long t = tid; t < T; t += kOrderNT) atomicAdd(&cnt[bucket(t)], 1);
-    __syncthreads();
-    // exclusive scan of the bucket counts (kOrderB == kOrderNT: one per thread)
-    const int c = cnt[tid];
-    int x = c;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < wv; ++w) base += wsum[w];
-    cnt[tid] = base + x - c;
-    __syncthreads();
-    for (long long t = tid; t < T; t += kOrderNT) order[atomicAdd(&cnt[bucket(t)], 1)] = (int)t;
-}
 #endif
 
 // ---------------------------------------------------------------- k_tables

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     constexpr int TPL = sorted_tail_per_lane(DIM), TCAP = sorted_tail_cap(DIM);
     const int n = S.n, tid = threadIdx.x, lane = tid & 63;
     const int ns = (n + 1) & ~1;                   // sorted_stride(n)
-    const long long t = P.order ? (long long)P.order[blockIdx.x] : (long long)blockIdx.x;   // dispatch order
+    const long long t = blockIdx.x;
     // One LDS region holds EITHER the generic tables (reference semantics: z, B, w per
     // axis; axis 0 of 3-D: w = the i1 == 0 weight) OR the fast records (16 B per axis
     // entry; 3-D axis 0 twice, [n, 2n) = the plane i1 == 0), chosen per date.
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     stamp(0);
     if (stamps && tid == 0) {
         stamps[25] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
-        stamps[30] = blockIdx.x;                         // dispatch position (cvq_plan_set_dispatch_order)
+        stamps[30] = blockIdx.x;                         // dispatch position (placement analysis)
         // placement: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of this workgroup's first wave
         stamps[27] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                      ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);

@@ -149,15 +149,6 @@ int32_t cvq_set_dates(cvq_plan* plan, int64_t T, const double* a, const double* 
  * counterpart (a launch-count optimisation of the device-resident path). */
 int32_t cvq_set_fast_hint(cvq_plan* plan, int32_t on);
 
-/* Dispatch order of the dates in the COMPACT / SORTED solves (no reference counterpart: the
- * reference's joblib pool, calc_integral.py:211, takes dates in index order).  mode 1: at each
- * cvq_set_dates a one-workgroup kernel (k_date_order) orders the batch by ascending predicted
- * portfolio scale sum_d (w_d sigma_td)^2 (MSM: sigma_td = sum_s f_tds sigma_ds), so the dates of
- * the heavy (-2, 0] bracket are dispatched first; mode 0: index order.  Results are identical
- * bit for bit (each date is solved independently); only the schedule changes.  Takes effect
- * at the next cvq_set_dates. */
-int32_t cvq_plan_set_dispatch_order(cvq_plan* plan, int32_t mode);
-
 /* Drop-in for ValueAtRiskCalcualtion.compute_integral (calc_var_class.py:179-212)
  * == calc_grids_and_integrals_results (calc_integral.py:8-119):
  * out[t] = integral of the joint copula density over the nested grid of

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/$tag
 mkdir -p $out
 timeout -k 10 500 python3 -u -m pytest tests/test_fullbatch_gpu.py tests/test_fullsize_oracle_gpu.py tests/test_gpu_parity.py \
-    tests/test_sorted_gpu.py tests/test_dispatch_order_gpu.py tests/test_sorted_width_gpu.py -m gpu -x -q \
+    tests/test_sorted_gpu.py tests/test_sorted_width_gpu.py -m gpu -x -q \
     --timeout 120 --timeout-method thread > $out/pytest.txt 2>&1 || { echo "pytest failed"; tail -30 $out/pytest.txt; exit 1; }
 tail -1 $out/pytest.txt
 for cd in "5 5000" "5 625" "3 5000" "2 1000"; do
