@@ -7,7 +7,7 @@ For one BASELINE workload at full size the plan runs, in this order, 3 x each of
 and prints the nodes the solve evaluates per date (device count).  `--report <dir>` then
 splits the solve's per-wave instruction counts into tables (A), node loops (nodes x the
 per-node cost from B - A) and the rest (levels, reductions, tails).
-usage: python3 tools/valu_split.py --config 5           (the run)
+usage: python3 tools/valu_split.py --config 5 [--strategy sorted]   (the run; mode-1 slabs need SORTED)
        python3 tools/valu_split.py --report <dir> --config 5 --nodes N --reach G --dates T
 """
 import argparse
@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "copula-msm-and-copula-garch-var_amd")]
 
 
-def run(cfg_no, T):
+def run(cfg_no, T, strategy):
     import numpy as np
     from copula_var import synthetic, tables
     from copula_var.engine import QuadraturePlan
@@ -38,7 +38,7 @@ def run(cfg_no, T):
         ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
     dens, x, step, combos = ggp
     p = QuadraturePlan(c.model, c.copula, c.dim, x, step, dens, combos, c.weights, c.copula_params(),
-                       vol_states=uvs, strategy="auto")
+                       vol_states=uvs, strategy=strategy)
     p.set_dates(ipt)
     T = c.T
     empty = np.tile([-100.0, -100.0], (T, 1))
@@ -87,10 +87,11 @@ if __name__ == "__main__":
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--dates", type=int, default=0)
     ap.add_argument("--report")
+    ap.add_argument("--strategy", default="sorted")
     ap.add_argument("--nodes", type=float)
     ap.add_argument("--reach", type=float)
     a = ap.parse_args()
     if a.report:
         report(a.report, a.nodes, a.reach, a.dates)
     else:
-        run(a.config, a.dates)
+        run(a.config, a.dates, a.strategy)
