@@ -30,6 +30,9 @@ Prints ONE JSON line (rank 0).
                   algorithmic bytes of §8d) over the same duration, and the PMC traffic.
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
+  other_configs -- (default cfg-2 run, rank 0, N=1) configs 5 / 3 / 4 at full size, each a child
+                  bench.py started after this run's timed legs: single solve (one batch at a
+                  time), kernel launch time, FP64 fraction, cfg 5's end to end; `--other-configs`.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  `python bench.py --gpus N` with no
 launcher around it starts its N ranks itself (torch.distributed.run as a child process, before
@@ -89,6 +92,10 @@ def parse():
     ap.add_argument("--nu", type=float, default=None,
                     help="Student copula nu instead of the config's (e.g. 5.364, an IFM-fitted value: the "
                          "non-integer node power path)")
+    ap.add_argument("--other-configs", default="auto",
+                    help="after the main line, run these BASELINE configs' single solves as child processes and "
+                         "attach their results (rank 0, N = 1): comma list, 'none', or 'auto' = 5,3,4 when the "
+                         "main config is 2")
     ap.add_argument("--time-all", type=int, default=0,
                     help="HIP-event time every kernel kind (adds event records to the timed region)")
     return ap.parse_args()
@@ -347,6 +354,10 @@ def main():
     if rank == 0 and world == 1 and a.cpu_baseline:
         cpu = cpu_baseline(c, ipt, uvs, ggp, ptf_mean, vals, a)
 
+    others = None
+    if rank == 0 and world == 1 and not strong:
+        others = other_configs(a)
+
     if rank == 0:
         kname = {"prefix": "k_mass (joint-mass row prefix)",
                  "direct": "k_direct (per-date slab-on-the-fly solve)",
@@ -405,12 +416,46 @@ def main():
             "var_checksum": float(np.nansum(vals)),
             "var_nan": int(np.isnan(vals).sum()),
             "cpu_baseline": cpu,
+            "other_configs": others,
         }
         print(json.dumps(out), flush=True)
     for p in plans:
         p.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def other_configs(a):
+    """The other BASELINE configs' single solves (one batch at a time, their full batches, auto
+    strategy; cfg 5 also end to end), each a fresh child `bench.py` process started after this
+    run's own timed legs, so the default run's line also carries them (SURVEY.md §8d lists
+    every config).  A child that fails or times out is recorded with its error, never raised."""
+    import subprocess
+    spec = a.other_configs
+    if spec == "none" or (spec == "auto" and (a.config != 2 or a.dates_per_gpu is not None or a.nu is not None
+                                              or a.strategy not in ("auto", "compact"))):
+        return None
+    cfgs = [5, 3, 4] if spec == "auto" else [int(v) for v in spec.split(",") if v.strip()]
+    res = {}
+    for cn in cfgs:
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", str(cn), "--inflight", "1", "--steps", "20",
+               "--warmup", "3", "--e2e", "1" if cn == 5 else "0", "--cpu-baseline", "0", "--other-configs", "none"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not line:
+                res[f"cfg{cn}"] = {"error": f"exit {r.returncode}: {r.stderr.strip().splitlines()[-1:] }"}
+                continue
+            d = json.loads(line[-1])
+            rf = d.get("roofline") or {}
+            res[f"cfg{cn}"] = {"workload": d["config"]["workload"], "strategy": d["config"]["strategy"],
+                               "dates": d["config"]["global_dates"], "single_solve": d["value"],
+                               "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+                               "kernel_avg_launch_us": rf.get("avg_launch_us"), "fp64_frac": rf.get("frac"),
+                               "e2e": (d.get("e2e") or {}).get("value"), "var_checksum": d.get("var_checksum")}
+        except subprocess.TimeoutExpired:
+            res[f"cfg{cn}"] = {"error": "timed out after 300 s"}
+    return res
 
 
 def end_to_end(a, c, block, per, plans, streams, vars_, args, vals, dev):

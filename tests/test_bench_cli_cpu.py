@@ -64,3 +64,37 @@ def test_mismatch_fails_before_torch_import():
                           "runpy.run_path('bench.py', run_name='__main__')"],
                          cwd=REPO, env=env, capture_output=True, text=True, timeout=60)
     assert out.returncode != 0 and "must agree" in out.stderr
+
+
+def test_other_configs_selection_and_record(monkeypatch):
+    """The default cfg-2 run attaches configs 5 / 3 / 4 as child bench runs (single solve, one
+    batch at a time); 'none', another main config or a scan argument turns them off; a failing
+    child is recorded, not raised."""
+    import json as _json
+    assert bench.other_configs(_args("--other-configs", "none")) is None
+    assert bench.other_configs(_args("--config", "5")) is None
+    assert bench.other_configs(_args("--dates-per-gpu", "500")) is None
+    calls = []
+
+    class R:
+        def __init__(self, rc, out, err=""):
+            self.returncode, self.stdout, self.stderr = rc, out, err
+
+    def fake_run(cmd, capture_output, text, timeout):
+        calls.append(cmd)
+        cn = int(cmd[cmd.index("--config") + 1])
+        if cn == 4:
+            return R(1, "", "boom\n")
+        line = {"value": 1.0e7 * cn, "unit": "VaR-dates/s", "ms_per_step": 0.2, "steps": 20, "var_checksum": -1.0,
+                "config": {"workload": f"cfg{cn}", "strategy": "compact", "global_dates": 5000},
+                "roofline": {"avg_launch_us": 180.0, "frac": 0.14}, "e2e": {"value": 9.9e6} if cn == 5 else None}
+        return R(0, "noise\n" + _json.dumps(line) + "\n")
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    res = bench.other_configs(_args())
+    assert set(res) == {"cfg5", "cfg3", "cfg4"}
+    assert res["cfg5"]["single_solve"] == 5.0e7 and res["cfg5"]["e2e"] == 9.9e6 and res["cfg5"]["fp64_frac"] == 0.14
+    assert res["cfg3"]["e2e"] is None
+    assert "error" in res["cfg4"]
+    assert all("--other-configs" in c and c[c.index("--other-configs") + 1] == "none" for c in calls)
+    assert all(c[c.index("--inflight") + 1] == "1" for c in calls)

@@ -15,7 +15,7 @@ passes=(
 i=0
 for p in "${passes[@]}"; do
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $out/p$i -o run -- \
-      python3 bench.py --cpu-baseline 0 --steps 5 --warmup 1 --e2e 0 --inflight 1 "$@" > $out/p$i.log 2>&1 \
+      python3 bench.py --cpu-baseline 0 --other-configs none --steps 5 --warmup 1 --e2e 0 --inflight 1 "$@" > $out/p$i.log 2>&1 \
       || { echo "pass $i failed rc=$?"; tail -3 $out/p$i.log; exit 1; }
   i=$((i+1))
 done

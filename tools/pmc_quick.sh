@@ -14,7 +14,7 @@ passes=(
 i=0
 for p in "${passes[@]}"; do
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $out/p$i -o run -- \
-      python3 bench.py --cpu-baseline 0 --steps 5 --warmup 1 "$@" > $out/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+      python3 bench.py --cpu-baseline 0 --other-configs none --steps 5 --warmup 1 "$@" > $out/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
   i=$((i+1))
 done
 python3 tools/pmc_summary.py $out "$@" > $out/summary.txt

@@ -15,7 +15,7 @@ for args in "$@"; do
   i=0
   for P in "$P0" "$P1"; do
     timeout -k 10 120 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $d/p$i -o run -- \
-        python3 bench.py --cpu-baseline 0 --steps 5 --warmup 1 --e2e 0 $args > $d.p$i.log 2>&1 \
+        python3 bench.py --cpu-baseline 0 --other-configs none --steps 5 --warmup 1 --e2e 0 $args > $d.p$i.log 2>&1 \
       || { echo "pmc case $k pass $i failed rc=$?"; tail -5 $d.p$i.log; exit 1; }
     i=$((i+1))
   done

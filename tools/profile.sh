@@ -8,6 +8,6 @@ cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o run -- \
-    python3 bench.py --cpu-baseline 0 "$@" > $out/bench.json 2> $out/stderr.log
+    python3 bench.py --cpu-baseline 0 --other-configs none "$@" > $out/bench.json 2> $out/stderr.log
 find $out -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
 ls -R $out | head -30
