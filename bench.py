@@ -31,8 +31,9 @@ Prints ONE JSON line (rank 0).
   cpu_baseline -- the joblib CPU path (oracle/joblib_port.py, scalar t.ppf),
                   timed on a bounded sample of the same workload, rank 0 at N=1.
   other_configs -- (default cfg-2 run, rank 0, N=1) configs 5 / 3 / 4 at full size, each a child
-                  bench.py started after this run's timed legs: single solve (one batch at a
-                  time), kernel launch time, FP64 fraction, cfg 5's end to end; `--other-configs`.
+                  bench.py started after this run's timed legs (20 steps): in flight, single solve
+                  (one batch at a time), kernel launch time, FP64 fraction, cfg 5's end to end;
+                  `--other-configs`.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  `python bench.py --gpus N` with no
 launcher around it starts its N ranks itself (torch.distributed.run as a child process, before
@@ -426,8 +427,8 @@ def main():
 
 
 def other_configs(a):
-    """The other BASELINE configs' single solves (one batch at a time, their full batches, auto
-    strategy; cfg 5 also end to end), each a fresh child `bench.py` process started after this
+    """The other BASELINE configs at full size (auto strategy): batches in flight, the single solve
+    (one batch at a time) and, for cfg 5, end to end -- each a fresh child `bench.py` process started after this
     run's own timed legs, so the default run's line also carries them (SURVEY.md §8d lists
     every config).  A child that fails or times out is recorded with its error, never raised."""
     import subprocess
@@ -438,7 +439,7 @@ def other_configs(a):
     cfgs = [5, 3, 4] if spec == "auto" else [int(v) for v in spec.split(",") if v.strip()]
     res = {}
     for cn in cfgs:
-        cmd = [sys.executable, os.path.abspath(__file__), "--config", str(cn), "--inflight", "1", "--steps", "20",
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", str(cn), "--steps", "20",
                "--warmup", "3", "--e2e", "1" if cn == 5 else "0", "--cpu-baseline", "0", "--other-configs", "none"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -449,7 +450,9 @@ def other_configs(a):
             d = json.loads(line[-1])
             rf = d.get("roofline") or {}
             res[f"cfg{cn}"] = {"workload": d["config"]["workload"], "strategy": d["config"]["strategy"],
-                               "dates": d["config"]["global_dates"], "single_solve": d["value"],
+                               "dates": d["config"]["global_dates"], "in_flight": d["value"],
+                               "inflight": d["config"]["inflight"],
+                               "single_solve": (d.get("single_solve") or {}).get("value"),
                                "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
                                "kernel_avg_launch_us": rf.get("avg_launch_us"), "fp64_frac": rf.get("frac"),
                                "e2e": (d.get("e2e") or {}).get("value"), "var_checksum": d.get("var_checksum")}

@@ -67,8 +67,8 @@ def test_mismatch_fails_before_torch_import():
 
 
 def test_other_configs_selection_and_record(monkeypatch):
-    """The default cfg-2 run attaches configs 5 / 3 / 4 as child bench runs (single solve, one
-    batch at a time); 'none', another main config or a scan argument turns them off; a failing
+    """The default cfg-2 run attaches configs 5 / 3 / 4 as child bench runs (in flight + single
+    solve); 'none', another main config or a scan argument turns them off; a failing
     child is recorded, not raised."""
     import json as _json
     assert bench.other_configs(_args("--other-configs", "none")) is None
@@ -85,8 +85,9 @@ def test_other_configs_selection_and_record(monkeypatch):
         cn = int(cmd[cmd.index("--config") + 1])
         if cn == 4:
             return R(1, "", "boom\n")
-        line = {"value": 1.0e7 * cn, "unit": "VaR-dates/s", "ms_per_step": 0.2, "steps": 20, "var_checksum": -1.0,
-                "config": {"workload": f"cfg{cn}", "strategy": "compact", "global_dates": 5000},
+        line = {"value": 2.0e7 * cn, "unit": "VaR-dates/s", "ms_per_step": 0.2, "steps": 20, "var_checksum": -1.0,
+                "single_solve": {"value": 1.0e7 * cn},
+                "config": {"workload": f"cfg{cn}", "strategy": "compact", "global_dates": 5000, "inflight": 3},
                 "roofline": {"avg_launch_us": 180.0, "frac": 0.14}, "e2e": {"value": 9.9e6} if cn == 5 else None}
         return R(0, "noise\n" + _json.dumps(line) + "\n")
 
@@ -97,4 +98,5 @@ def test_other_configs_selection_and_record(monkeypatch):
     assert res["cfg3"]["e2e"] is None
     assert "error" in res["cfg4"]
     assert all("--other-configs" in c and c[c.index("--other-configs") + 1] == "none" for c in calls)
-    assert all(c[c.index("--inflight") + 1] == "1" for c in calls)
+    assert res["cfg5"]["in_flight"] == 1.0e8
+    assert all("--inflight" not in c for c in calls)                  # the default batches in flight
