@@ -1488,51 +1488,46 @@ __device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const 
     return true;
 }
 
-// Forecast-only UKF pass (k_ukf_forecast, k_ukf_sigma): ukf_pass's recursion with the step's
-// dependent chain shortened -- w / exp(X) as w * exp(-X), the three (.) / Z and (h / Z) of the
-// update as one reciprocal of Z (v_rcp_f64 + two Newton steps, ~1 ulp) times the sums, no
-// log-likelihood -- so a step waits on one reciprocal instead of two IEEE division stages
-// (one window per thread, ~150 waves on the chip: the forecast is latency-bound).  A few ulp
-// per step; the filter contracts, and sigma stays within 1e-12 of the reference's goldens
-// (tests/test_gpu_parity.py).  Same failure rule as ukf_pass (estimate.py:219-220, :270-271).
+// Forecast-only UKF pass (k_ukf_forecast, k_ukf_sigma): ukf_pass's recursion (estimate.py:230-281)
+// with each step's dependent chain shortened, one window per thread (~150 waves on the chip, so
+// the forecast is latency-bound):
+//  * prediction in closed form: the five sigma points x + phi (0, +c0, 0, -c0, 0), noise
+//    phi (0, 0, 1, 0, -1) through f = a (x - l) + l + q noise have the weighted mean
+//    a (x - l) + l (wm0 + 4 wm1 = 1) and the covariance 2 wc1 phi^2 (a^2 dvar + q^2) -- no
+//    square root of dvar on the chain;
+//  * update about the predicted mean: with y = X2 - xm in {0, +phi sP, -phi sP}, the weighted
+//    sums Z, Sy, Syy of (h, h y, h y^2) are independent, mean = xm + Sy / Z and the variance
+//    Syy / Z - (Sy / Z)^2 (no second pass over the points); w / exp(X) as w * exp(-X) and one
+//    reciprocal of Z (v_rcp_f64 + two Newton steps, ~1 ulp).
+// The algebra is exact, the rounding differs from the sigma-point arithmetic by a few ulp per
+// step; the filter contracts, and sigma stays within 1e-12 of the reference's goldens
+// (tests/test_gpu_parity.py, tests/test_insample_gpu.py).  Same failure rule as ukf_pass
+// (estimate.py:219-220, :270-271).
 __device__ bool ukf_forecast_pass(const UkfConst& C, double a, double l, double q, const double* w, long long N,
                                   double* xmean_last) {
-    double x = l, var = q;
+    double x = l, var = q;                                        // forecast.py:9: init (l, q)
     double xm = 0.0;
+    const double kP = 2.0 * C.wc1 * (C.phi * C.phi), a2 = a * a, q2 = q * q;
     for (long long t = 0; t < N; ++t) {
-        const double dvar = (var <= 0) ? var + 1e-8 : var;
-        const double c0 = sqrt(dvar);
-        const double X1a[5] = {x, x + C.phi * c0, x + C.phi * 0.0, x - C.phi * c0, x - C.phi * 0.0};
-        const double X1b[5] = {0.0, 0.0 + C.phi * 0.0, 0.0 + C.phi * 1.0, 0.0 - C.phi * 0.0, 0.0 - C.phi * 1.0};
-        double X[5];
-        for (int i = 0; i < 5; ++i) X[i] = a * (X1a[i] - l) + l + q * X1b[i];
-        xm = X[0] * C.wm0;
-        for (int i = 1; i < 5; ++i) xm += X[i] * C.wm1;
-        double P = 0.0;
-        for (int i = 0; i < 5; ++i) {
-            const double d = X[i] - xm;
-            P += (d * (i == 0 ? C.wc0 : C.wc1)) * d;
-        }
-        const double sP = sqrt(P);
-        const double X2[3] = {xm, xm + C.phi * sP, xm - C.phi * sP};
+        const double dvar = (var <= 0) ? var + 1e-8 : var;        // custom_cholesky :72-74
+        xm = a * (x - l) + l;
+        const double sP = sqrt(kP * fma(a2, dvar, q2));
+        const double y[3] = {0.0, C.phi * sP, -(C.phi * sP)};
         const double wt = w[t];
-        double h[3], Z = 0.0, S1 = 0.0;
+        double Z = 0.0, Sy = 0.0, Syy = 0.0;
         for (int i = 0; i < 3; ++i) {
-            const double eta = wt * exp(-X2[i]);
-            h[i] = (kInvSqrt2Pi * exp(-0.5 * (eta * eta))) * fabs(eta);
-            const double wi = (i == 0 ? C.wm2_0 : C.wm2_1) * h[i];
+            const double eta = wt * exp(-(xm + y[i]));
+            const double h = (kInvSqrt2Pi * exp(-0.5 * (eta * eta))) * fabs(eta);
+            const double wi = (i == 0 ? C.wm2_0 : C.wm2_1) * h;
             Z += wi;
-            S1 += wi * X2[i];
+            Sy = fma(wi, y[i], Sy);
+            Syy = fma(wi * y[i], y[i], Syy);
         }
         if (Z <= 0 || Z < 1e-10) return false;
         const double rz = fast_rcp(Z);
-        const double mean = S1 * rz;
-        double S2 = 0.0;
-        for (int i = 0; i < 3; ++i) {
-            const double d = X2[i] - mean;
-            S2 += ((i == 0 ? C.wm2_0 : C.wm2_1) * h[i]) * (d * d);
-        }
-        const double v2 = S2 * rz;
+        const double mu = Sy * rz;
+        const double mean = xm + mu;
+        const double v2 = fma(Syy, rz, -(mu * mu));
         if (isnan(mean) || isnan(v2) || isnan(Z)) return false;
         x = mean;
         var = v2;
