@@ -32,7 +32,7 @@ Prints ONE JSON line (rank 0).
                   timed on a bounded sample of the same workload, rank 0 at N=1.
   other_configs -- (default cfg-2 run, rank 0, N=1) configs 5 / 3 / 4 at full size, each a child
                   bench.py started after this run's timed legs (20 steps): in flight, single solve
-                  (one batch at a time), kernel launch time, FP64 fraction, cfg 5's end to end;
+                  (one batch at a time), kernel launch time, FP64 fraction, end to end;
                   `--other-configs`.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  `python bench.py --gpus N` with no
@@ -428,7 +428,7 @@ def main():
 
 def other_configs(a):
     """The other BASELINE configs at full size (auto strategy): batches in flight, the single solve
-    (one batch at a time) and, for cfg 5, end to end -- each a fresh child `bench.py` process started after this
+    (one batch at a time) and end to end -- each a fresh child `bench.py` process started after this
     run's own timed legs, so the default run's line also carries them (SURVEY.md §8d lists
     every config).  A child that fails or times out is recorded with its error, never raised."""
     import subprocess
@@ -440,7 +440,7 @@ def other_configs(a):
     res = {}
     for cn in cfgs:
         cmd = [sys.executable, os.path.abspath(__file__), "--config", str(cn), "--steps", "20",
-               "--warmup", "3", "--e2e", "1" if cn == 5 else "0", "--cpu-baseline", "0", "--other-configs", "none"]
+               "--warmup", "3", "--e2e", "1", "--cpu-baseline", "0", "--other-configs", "none"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -86,8 +86,9 @@ class ShardedVaR:
         bisection budget after the finalize (synchronises; the status is global, from
         the gathered headers, so every rank raises together)."""
         self._local(self.hdr, self.snaps)
-        blocks = self.block.view(1, -1) if self.world == 1 else _gather(self.block.view(1, -1), self.world,
-                                                                        self.group)
+        # a process group of one still takes the collective (the path every N > 1 run takes)
+        blocks = (self.block.view(1, -1) if not dist.is_initialized()
+                  else _gather(self.block.view(1, -1), self.world, self.group))
         self._finalize(blocks, self.var)
         if check and self._check is not None:
             self._check()

@@ -29,8 +29,10 @@ def solve_args(ptf_mean: float = 0.0, obj_var=0.05, first_guess=-3.0, second_gue
                           float(min_var), float(max_var), float(lower), float(tolerance), float(ptf_mean))
 
 
-MAX_N = 512                           # num_points limit of every plan (cvq_plan_create)
-SORTED_MAX_N = {2: 512, 3: 255}      # sorted_max_n (cvq_sorted_kernels.h)
+MAX_N = 512                           # num_points limit of every strategy but 2-D SORTED (cvq_plan_create)
+SORTED_MAX_N = {2: 1024, 3: 255}     # sorted_max_n (cvq_sorted_kernels.h): 2-D n > 512 runs 1024-thread dates;
+                                      # 3-D: the 32-bit node word (a0 = i0 + n [i1 == 0] < 2n in 9 bits,
+                                      # i1 in 8); its LDS (9 n doubles + a 16-KB tail) is not the bound
 PREFIX_MAX_N_3D = 64                  # PREFIX solves at most 4096 rows (cvq_plan.hip pick_solve_shape)
 MATERIALISED = ("prefix", "sorted", "sweep")   # strategies that hold only nodes with level <= v_cap
 
@@ -54,12 +56,17 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None, copula: Optiona
     for 3 assets (the only strategy that runs the 128^3 grid of cfg 4).  n (num_points)
     bounds the choice: every 2-D strategy takes n <= 512 (the plan's limit, so a 2-D
     rule never picks a strategy that fails later), 3-D SORTED n <= 255, 3-D PREFIX n <= 64; no 3-D strategy
-    takes n > 255.  SORTED and PREFIX hold the nodes with level <= v_cap only;
+    takes n > 255.  A 2-D grid with 512 < n <= 1024 (the reference takes any num_points,
+    calc_var_class.py:16; main.py:50 suggests raising it) runs on SORTED, whose 1024-thread
+    instance holds it.  SORTED and PREFIX hold the nodes with level <= v_cap only;
     QuadraturePlan(strategy="auto") routes a query above v_cap to an unrestricted
-    sibling plan (COMPACT / DIRECT in 2-D, SORTED with v_cap at the grid's top in 3-D)."""
+    sibling plan (COMPACT in 2-D, SORTED with v_cap at the grid's top in 3-D and for
+    2-D n > 512)."""
     if dim == 2:
         if n is not None and n > MAX_N:
-            raise ValueError(f"num_points <= {MAX_N} (every strategy: cvq_plan_create), got {n}")
+            if n > SORTED_MAX_N[2]:
+                raise ValueError(f"2-asset grids support num_points <= {SORTED_MAX_N[2]} (SORTED), got {n}")
+            return "sorted"
         # a fitted (non-integer) Student nu: SORTED (cfg 2 at nu = 5.364: 9.4M vs COMPACT 7.8M
         # VaR-dates/s; COMPACT's general-power instance needs 104 VGPRs, 4 waves per SIMD)
         if general_power(copula, copula_params):
@@ -108,6 +115,7 @@ class QuadraturePlan:
         self._dates = None                                  # last set_dates / set_dates_device arguments
         self._stream, self._timing, self._counting = None, False, False   # forwarded to the sibling
         self._last: Optional["QuadraturePlan"] = None       # plan of the last device solve (solve_status)
+        self._counted: Optional["QuadraturePlan"] = None    # plan that ran the last solve / slab (node counts)
         if strategy == "auto":
             strategy = auto_strategy(model, self.dim, self._x.size, copula, self._cp)
         st.strategy = {"prefix": N.STRATEGY_PREFIX, "direct": N.STRATEGY_DIRECT,
@@ -147,14 +155,15 @@ class QuadraturePlan:
             self._wide = None
         if self._wide is None:
             model, copula, dim, x, step, dens, combos, w, cp, vs, dev = self._ctor
-            if self.dim == 2:
+            if self.dim == 2 and self._x.size <= MAX_N:
                 self._wide = QuadraturePlan(model, copula, dim, x, step, dens, combos, w, cp, vol_states=vs,
                                             device=dev, strategy="compact")
             else:
                 grid_top = float(np.sum(np.abs(self._w)) * np.max(np.abs(self._x)))
                 self._wide = QuadraturePlan(model, copula, dim, x, step, dens, combos, w, cp, vol_states=vs,
                                             v_cap=max(grid_top, float(top)), device=dev, strategy="sorted")
-            self._wide.set_stream(self._stream)
+            if self._stream is not None:          # else the sibling keeps its own non-blocking stream
+                self._wide.set_stream(self._stream)
             if self._dates is not None:
                 kind, args = self._dates
                 (self._wide.set_dates if kind == "host" else self._wide.set_dates_device)(*args)
@@ -220,8 +229,8 @@ class QuadraturePlan:
     def nodes_evaluated(self) -> int:
         """Nodes evaluated by the last counted solve, summed over its dates (read from the
         sibling plan when the auto rule routed that solve there)."""
-        if self._last is not None and self._last is not self:
-            return self._last.nodes_evaluated()
+        if self._counted is not None and self._counted is not self:
+            return self._counted.nodes_evaluated()
         n = C.c_int64()
         N.check(N.lib().cvq_plan_nodes_evaluated(self._h, C.byref(n)), "cvq_plan_nodes_evaluated")
         return int(n.value)
@@ -271,6 +280,7 @@ class QuadraturePlan:
             raise ValueError(f"bounds must have shape ({self.T}, 2)")
         top = float(np.nanmax(b)) if b.size else 0.0
         target = self._route(top)
+        self._counted = target
         if target is not self:
             return target.compute_integral(b)
         out = np.empty(self.T)
@@ -282,7 +292,7 @@ class QuadraturePlan:
         """Drop-in for calc_var (calc_var_class.py:95-177): returns (VaR (T,), iterations)."""
         args = solve_args(ptf_mean, obj_var, first_guess, second_guess, **consts)
         target = self._route(self._top(args))
-        self._last = target
+        self._last = self._counted = target
         if target is not self:
             return target.calc_var(ptf_mean, obj_var, first_guess, second_guess, **consts)
         out = np.empty(self.T)
@@ -298,7 +308,7 @@ class QuadraturePlan:
         iterations (non-dyadic guesses) and returns the iteration count.  A plan built with
         strategy "auto" routes levels above v_cap to its unrestricted sibling, as calc_var does."""
         target = self._route(self._top(args))
-        self._last = target
+        self._last = self._counted = target
         if target is not self:
             return target.solve_device(args, var_ptr, check)
         if not check:
@@ -328,6 +338,7 @@ class QuadraturePlan:
     def solve_local(self, args: N.CvqSolveArgs, header_ptr: int, snaps_ptr: int) -> None:
         target = self._route(self._top(args))
         self._last = None                        # the finalize (on this plan) reports the status
+        self._counted = target
         if target is not self:
             return target.solve_local(args, header_ptr, snaps_ptr)
         N.check(N.lib().cvq_solve_local(self._h, C.byref(args), C.c_void_p(header_ptr), C.c_void_p(snaps_ptr)),

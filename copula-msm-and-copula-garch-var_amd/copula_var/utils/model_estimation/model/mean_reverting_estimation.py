@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .... import insample, tables
+from .... import insample, integrand, tables
 from ....data_loader.load_data import centred_series
 from ...calc_var_ABC import SharedCacheCopulaMRVaR, VaRCalculationMethod
 from .garch_estimation import GarchEstimation
@@ -68,5 +68,11 @@ class MeanRevertingEstimation(VaRCalculationMethod):
         n_in = centred.shape[0] - len(rolling_windows_dict)
         return tables.sigma_integration_params(centred, n_in, "mean_reverting", params, num_points, self.device)
 
-    def integrated_function(self, *args, **kwargs):
-        raise NotImplementedError("the integrand is evaluated inside the device quadrature (cvq_slab / cvq_solve)")
+    def integrated_function(self, grids, step_sizes, copula_params, integrations_params_i,
+                            integrations_params_static, copula_density, unpack_copula_params):
+        """garch_integration_function.py:5-52 (mean_reverting_estimation.py:235-253): the per-node integrand for a caller-built
+        nested grid, erf / quantiles on this adapter's device (copula_var/integrand.py).  The VaR
+        path does not use it: the device solve evaluates the integrand in its kernels."""
+        return integrand.sigma_integrated_function(grids, step_sizes, copula_params, integrations_params_i,
+                                                    integrations_params_static, copula_density,
+                                                    unpack_copula_params, device=self.device)

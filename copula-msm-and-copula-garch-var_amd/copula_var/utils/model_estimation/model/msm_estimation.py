@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .... import insample, tables
+from .... import insample, integrand, tables
 from ....data_loader.load_data import centred_series
 from ...calc_var_ABC import SharedCacheCopulaMSMVaR, VaRCalculationMethod
 
@@ -96,5 +96,11 @@ class MSMEstimation(VaRCalculationMethod):
     def compute_forecast_combinations(forecasts_by_states):
         return tables.forecast_combinations(np.asarray(forecasts_by_states))
 
-    def integrated_function(self, *args, **kwargs):
-        raise NotImplementedError("the integrand is evaluated inside the device quadrature (cvq_slab / cvq_solve)")
+    def integrated_function(self, grids, step_sizes, copula_params, integrations_params_i,
+                            integrations_params_static, copula_density, unpack_copula_params):
+        """msm_integration_function.py:5-47 (msm_estimation.py:445-454): the per-node integrand for a caller-built
+        nested grid, erf / quantiles on this adapter's device (copula_var/integrand.py).  The VaR
+        path does not use it: the device solve evaluates the integrand in its kernels."""
+        return integrand.msm_integrated_function(grids, step_sizes, copula_params, integrations_params_i,
+                                                    integrations_params_static, copula_density,
+                                                    unpack_copula_params, device=self.device)

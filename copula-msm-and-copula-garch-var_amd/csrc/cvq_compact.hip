@@ -9,6 +9,7 @@ namespace cvq {
 
 int compact_max_n() { return 2 * CVQ_COMPACT_NT; }      // 1 or 2 rows per thread (launch_f)
 int compact_tail_cap() { return CVQ_COMPACT_NT * kBlkPerThread; }   // block tail: cell nodes per workgroup
+int compact_nt() { return CVQ_COMPACT_NT; }
 
 int launch_compact(const StaticDev& S, const SolveConst& P, const CompactGeom& G, long long T, hipStream_t stream,
                    const double* a, const double* tA, const double* tB, const double* pi, bool fused, double* st,

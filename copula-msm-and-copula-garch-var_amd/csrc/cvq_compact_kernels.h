@@ -121,6 +121,11 @@ struct CompactGeom {
     // with ccount: [4][2^cdepth][n] per-row cuts cnt_r(mid) of every bisection cell the levels split
     // (heap nodes 1 .. 2^cdepth - 1; date-independent, host-built); nullptr: the levels search the grid
     const int16_t* kcut;
+    // [3][NT RPT] the fixed slabs' schedule: slot tid + NT k sums two half-rows of slab (lower, fg],
+    // (sg0, fg] or (fg, sg1], int16 codes 2 r + h (h = 1: the second half of row r; -1: none) in the
+    // low / high half-word, host-paired longest with shortest (ensure_cutfix); nullptr: slot k of
+    // thread tid takes the first half of row r and the second half of row n - 1 - r
+    const int* fpair;
 };
 
 // ------------------------------------------------------------------ reductions
@@ -555,6 +560,12 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int w = min(tid + NT * k, (kCutLds / 2) * n - 1);
         cv[k] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
     }
+    // the fixed slabs' half-row pairs (host schedule G.fpair): (lower, fg], (sg0, fg], (fg, sg1]
+    int fpv[3][RPT];
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) fpv[s3][k] = G.fpair ? G.fpair[s3 * NT * RPT + tid + NT * k] : 0;
     // the first bisection level's per-row cuts of all four brackets (host table G.kcut, heap node 1)
     int krt[4][RPT];
 #pragma unroll
@@ -724,8 +735,32 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // slab (va, vb] between two fixed levels: these are triangles and corner bands
     // whose row lengths run from 0 to ~n, so the owner of row r sums the first half
     // of row r and the second half of row n - 1 - r (long rows pair with short ones)
-    auto fixed_slab = [&](double va, double vb) {
+    // sl: the slab's host schedule (0 = (lower, fg], 1 = (sg0, fg], 2 = (fg, sg1]; -1: none)
+    auto fixed_slab = [&](double va, double vb, int sl) {
         double part = 0.0;
+        if (G.fpair && sl >= 0) {
+            auto cut = [&](const int16_t* c, double v) {
+                return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
+                     : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : c[kCutVmax];
+            };
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                const int w = sl == 0 ? fpv[0][k] : sl == 1 ? fpv[1][k] : fpv[2][k];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int code = (int)(int16_t)(e == 0 ? (w & 0xFFFF) : ((unsigned)w >> 16));
+                    if (code < 0) continue;
+                    const int r = code >> 1;
+                    const int16_t* c = cfx + (size_t)r * kCutLds;
+                    const int a = cut(c, va), b = max((int)cut(c, vb), a), m = a + (b - a + 1) / 2;
+                    const int j0 = (code & 1) ? m + 1 : a + 1, j1 = (code & 1) ? b : m;
+                    if (j1 >= j0) part += range_sum(r, j0, j1);
+                    nev += max(j1 - j0 + 1, 0);
+                }
+            }
+            sums[0] = team_sum1<NT>(part, red, parity);
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             if (!own[k]) continue;
@@ -747,13 +782,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    fixed_slab(P.lower, P.fg);
+    fixed_slab(P.lower, P.fg, 0);
     const double r0 = sums[0];
     stamp(2);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    fixed_slab(nl, nu);
+    fixed_slab(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1);
     const double nr = sums[0];
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);

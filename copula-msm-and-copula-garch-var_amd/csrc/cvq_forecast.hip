@@ -1496,9 +1496,13 @@ __device__ bool ukf_pass(const UkfConst& C, double a, double l, double q, const 
 //    a (x - l) + l (wm0 + 4 wm1 = 1) and the covariance 2 wc1 phi^2 (a^2 dvar + q^2) -- no
 //    square root of dvar on the chain;
 //  * update about the predicted mean: with y = X2 - xm in {0, +phi sP, -phi sP}, the weighted
-//    sums Z, Sy, Syy of (h, h y, h y^2) are independent, mean = xm + Sy / Z and the variance
-//    Syy / Z - (Sy / Z)^2 (no second pass over the points); w / exp(X) as w * exp(-X) and one
-//    reciprocal of Z (v_rcp_f64 + two Newton steps, ~1 ulp).
+//    sums Z, Sy of (h, h y) are independent, mean = xm + Sy / Z; w / exp(X) as w * exp(-X) and
+//    one reciprocal of Z (v_rcp_f64 + two Newton steps, ~1 ulp);
+//  * the variance as the reference forms it, a sum of non-negative terms about the updated
+//    mean, sum w_i h_i (y_i - mu)^2 / Z (estimate.py:226).  The shortcut Syy / Z - mu^2 cancels
+//    when one sigma point carries nearly all the weight (a return far in the tail): it can round
+//    below 0 and take custom_cholesky's var <= 0 -> +1e-8 branch (:72-74) where the reference's
+//    variance is a tiny positive number (tests/test_ukf_variance_gpu.py pins that regime).
 // The algebra is exact, the rounding differs from the sigma-point arithmetic by a few ulp per
 // step; the filter contracts, and sigma stays within 1e-12 of the reference's goldens
 // (tests/test_gpu_parity.py, tests/test_insample_gpu.py).  Same failure rule as ukf_pass
@@ -1514,20 +1518,21 @@ __device__ bool ukf_forecast_pass(const UkfConst& C, double a, double l, double 
         const double sP = sqrt(kP * fma(a2, dvar, q2));
         const double y[3] = {0.0, C.phi * sP, -(C.phi * sP)};
         const double wt = w[t];
-        double Z = 0.0, Sy = 0.0, Syy = 0.0;
+        double Z = 0.0, Sy = 0.0, wv[3];
         for (int i = 0; i < 3; ++i) {
             const double eta = wt * exp(-(xm + y[i]));
             const double h = (kInvSqrt2Pi * exp(-0.5 * (eta * eta))) * fabs(eta);
             const double wi = (i == 0 ? C.wm2_0 : C.wm2_1) * h;
+            wv[i] = wi;
             Z += wi;
             Sy = fma(wi, y[i], Sy);
-            Syy = fma(wi * y[i], y[i], Syy);
         }
         if (Z <= 0 || Z < 1e-10) return false;
         const double rz = fast_rcp(Z);
         const double mu = Sy * rz;
         const double mean = xm + mu;
-        const double v2 = fma(Syy, rz, -(mu * mu));
+        const double d1 = y[1] - mu, d2 = y[2] - mu;
+        const double v2 = fma(wv[0] * mu, mu, fma(wv[1] * d1, d1, (wv[2] * d2) * d2)) * rz;
         if (isnan(mean) || isnan(v2) || isnan(Z)) return false;
         x = mean;
         var = v2;

@@ -108,6 +108,7 @@ int make_tconst(double nu, TConst* tk, double** d_cf) {
 }
 
 int compact_tail_cap();                      // cvq_compact.hip: the block tail's node capacity
+int compact_nt();                            // cvq_compact.hip: threads per COMPACT workgroup
 }  // namespace cvq
 
 using namespace cvq;
@@ -166,6 +167,7 @@ struct cvq_plan {
     int bstart[4] = {0, 0, 0, 0};   // ub(bracket lower) in hvc for the cached solve arguments
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
+    int* d_fpair = nullptr;      // [3][NT RPT] COMPACT fixed slabs' half-row pairs per thread slot
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -706,6 +708,7 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     const double key[6] = {P.lower, P.sg0, P.fg, P.sg1, P.vmin, P.vmax};
     if (p->cut_valid && std::memcmp(key, p->cut_key, sizeof key) == 0) return CVQ_OK;
     const int n = p->S.n;
+    int rc0 = CVQ_OK;
     std::vector<int16_t> h((size_t)n * kCutFixed, 0);
     for (int r = 0; r < n; ++r) {
         const double lev = p->hx[r] * p->S.w1;
@@ -714,6 +717,36 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     p->cut_valid = false;
     if (!p->d_cutfix) CVQ_HIP_CHECK(hipMalloc((void**)&p->d_cutfix, h.size() * sizeof(int16_t)));
     CVQ_HIP_CHECK(hipMemcpyAsync(p->d_cutfix, h.data(), h.size() * sizeof(int16_t), hipMemcpyHostToDevice, p->stream));
+    // COMPACT's fixed slabs (lower, fg], (sg0, fg], (fg, sg1]: each thread slot sums two half-rows
+    // (the first or second half of a row's column range).  Sorted by length and paired longest with
+    // shortest, a wave's lanes carry similar work (the fixed slabs are triangles and corner bands:
+    // row lengths run from 0 to ~n, and the loops run to the wave's longest lane); any assignment
+    // that takes every half-row once gives the same slab, so this is a schedule, not a semantics.
+    {
+        const int NT = compact_nt(), M = NT * ((n + NT - 1) / NT);
+        std::vector<int> fp((size_t)3 * M);
+        const int cols[3][2] = {{kCutLower, kCutFg}, {kCutSg0, kCutFg}, {kCutFg, kCutSg1}};
+        std::vector<std::pair<int, int>> hl((size_t)2 * M);
+        for (int sl = 0; sl < 3; ++sl) {
+            for (int r = 0; r < n; ++r) {
+                const int a = h[(size_t)r * kCutFixed + cols[sl][0]];
+                const int b = std::max<int>(h[(size_t)r * kCutFixed + cols[sl][1]], a);
+                const int m = a + (b - a + 1) / 2;
+                hl[2 * r] = {m - a, 2 * r};                  // first half (a, m]
+                hl[2 * r + 1] = {b - m, 2 * r + 1};          // second half (m, b]
+            }
+            for (int e = 2 * n; e < 2 * M; ++e) hl[e] = {-1, -1};   // no half-row
+            std::stable_sort(hl.begin(), hl.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+                return x.first > y.first;
+            });
+            for (int e = 0; e < M; ++e) {
+                const int ca = hl[e].second, cb = hl[2 * M - 1 - e].second;
+                fp[(size_t)sl * M + e] = (int)((uint32_t)(ca & 0xFFFF) | ((uint32_t)(cb & 0xFFFF) << 16));
+            }
+        }
+        if (!p->d_fpair && (rc0 = dev_alloc(&p->d_fpair, fp.size()))) return rc0;
+        CVQ_HIP_CHECK(hipMemcpyAsync(p->d_fpair, fp.data(), fp.size() * sizeof(int), hipMemcpyHostToDevice, p->stream));
+    }
     std::vector<int> cc;
     build_cell_counts(p->hvc, P, compact_tail_cap(), cc, &p->ccount_depth);
     const double blo[4] = {P.vmin, P.sg0, P.sg1, P.fg};      // k_compact's brackets' lower levels
@@ -865,10 +898,12 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
             p->capDefer = p->T + 2;
         }
         const bool tab = p->ccount_depth >= 0;
+        // CVQ_FPAIR=0: the fixed slabs' (r, n - 1 - r) half-row pairing instead of the host schedule (A/B)
+        static const bool fpair_sched = !(getenv("CVQ_FPAIR") && atoi(getenv("CVQ_FPAIR")) == 0);
         const CompactGeom G{p->d_cutfix, p->d_vstar, p->d_bucket, p->bx0, p->binv, p->nb,
                             tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
                             {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]},
-                            (tab && p->kcut_ok) ? p->d_kcut : nullptr};
+                            (tab && p->kcut_ok) ? p->d_kcut : nullptr, fpair_sched ? p->d_fpair : nullptr};
         return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
@@ -1124,7 +1159,9 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
     CVQ_REQUIRE(s->dim == 2 || s->dim == 3, CVQ_ERR_UNSUPPORTED, "dim must be 2 or 3");
     CVQ_REQUIRE(!(s->copula == CVQ_PLACKETT && s->dim != 2), CVQ_ERR_UNSUPPORTED,
                 "Plackett copula is only defined for 2-dimensional marginals (plackett.py:20-21)");
-    CVQ_REQUIRE(s->n >= 2 && s->n <= 512, CVQ_ERR_UNSUPPORTED, "num_points must be in [2, 512]");
+    CVQ_REQUIRE(s->n >= 2 && s->n <= 1024, CVQ_ERR_UNSUPPORTED, "num_points must be in [2, 1024]");
+    CVQ_REQUIRE(s->n <= 512 || (s->strategy == CVQ_STRATEGY_SORTED && s->dim == 2), CVQ_ERR_UNSUPPORTED,
+                "num_points > 512 needs the SORTED strategy in 2-D (every strategy takes n <= 512)");
     CVQ_REQUIRE(s->q >= 1 && s->q <= kMaxQ, CVQ_ERR_UNSUPPORTED, "q (unique vol states) must be in [1, 8]");
     int Q = 1;
     for (int d = 0; d < s->dim; ++d) Q *= s->q;
@@ -1343,7 +1380,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_fpair, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_pass,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
@@ -1376,6 +1413,7 @@ int32_t cvq_plan_timing(cvq_plan* p, int32_t enable) {
 int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_t* launches) {
     cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && total_ms != nullptr && launches != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));          // the plan's device (its stream and buffers)
     CVQ_REQUIRE(kind >= 0 && kind < TK_COUNT, CVQ_ERR_INVALID, "unknown kernel kind");
     double tot = 0.0;
     int cnt = 0;
@@ -1395,6 +1433,7 @@ int32_t cvq_plan_kernel_time(cvq_plan* p, int32_t kind, double* total_ms, int32_
 int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
     cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));          // the plan's device (its stream and buffers)
     CVQ_REQUIRE(p->d_stamps != nullptr, CVQ_ERR_STATE, "no stamps recorded (set CVQ_STAMPS=1; DIRECT, COMPACT or SORTED strategy)");
     CVQ_REQUIRE(count <= p->capStamps * 32, CVQ_ERR_INVALID, "count exceeds the stamp buffer");
     CVQ_HIP_CHECK(hipStreamSynchronize(p->stream));
@@ -1405,6 +1444,7 @@ int32_t cvq_plan_debug_stamps(cvq_plan* p, uint64_t* host, int64_t count) {
 int32_t cvq_plan_debug_nodes(cvq_plan* p, uint32_t* host, int64_t count, int32_t* fix) {
     cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && host != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));          // the plan's device (its stream and buffers)
     CVQ_REQUIRE(p->d_pidx != nullptr && p->tree_valid, CVQ_ERR_STATE,
                 "no solve-order node list (a SORTED plan builds it at its first solve)");
     CVQ_REQUIRE(count >= 0 && count <= (int64_t)p->S.G, CVQ_ERR_INVALID, "count must be in [0, reachable nodes]");
@@ -1436,6 +1476,7 @@ int32_t cvq_plan_count_nodes(cvq_plan* p, int32_t enable) {
 int32_t cvq_plan_nodes_evaluated(cvq_plan* p, int64_t* total) {
     cvq::DeviceScope device_scope;                 // the caller's current device, restored on return
     CVQ_REQUIRE(p != nullptr && total != nullptr, CVQ_ERR_INVALID, "NULL argument");
+    CVQ_HIP_CHECK(hipSetDevice(p->device));          // the plan's device (its stream and buffers)
     CVQ_REQUIRE(p->nodes_valid && p->d_stamps != nullptr, CVQ_ERR_STATE,
                 "no node counts recorded (cvq_plan_count_nodes(plan, 1), then cvq_solve)");
     std::vector<unsigned long long> h((size_t)p->T * 32);

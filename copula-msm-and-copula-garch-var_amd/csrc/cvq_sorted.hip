@@ -34,13 +34,15 @@ int device_cus() {
 // (625 dates: 384 threads, every workgroup resident) measured slower than 512 threads with the
 // last ~100 dates starting late (cfg 3 133 vs 116 us, cfg 5 118 vs 103 us; profiles/r04o).
 // CVQ_SORT_NT (256 / 384 / 512 / 1024) overrides (A/B).
-int sorted_threads(long long T, int dim) {
+// A 2-D grid with n > 512 needs the 1024-thread instance (sorted_max_n_nt).
+int sorted_threads(long long T, int dim, int n) {
+    const int nt_min = n > sorted_max_n_nt(dim, kSortNT) ? 1024 : kSortNT;
     const char* ev = getenv("CVQ_SORT_NT");            // read per launch: tests switch it per case
     const int env = ev ? atoi(ev) : 0;
-    if (env == 256 || env == 384 || env == 512 || env == 1024) return env;
-    for (int nt = 1024; nt > kSortNT; nt >>= 1)
+    if ((env == 256 || env == 384 || env == 512 || env == 1024) && env >= nt_min) return env;
+    for (int nt = 1024; nt > nt_min; nt >>= 1)
         if (T * (nt / 64) <= (long long)device_cus() * 4 * sorted_min_waves(dim, nt)) return nt;
-    return kSortNT;
+    return nt_min;
 }
 
 int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, long long T, hipStream_t stream,
@@ -49,9 +51,10 @@ int launch_sorted(const StaticDev& S, const SolveConst& P, const SortedGeom& G, 
                   size_t abi) {
     CVQ_REQUIRE(abi == (kernel_abi_key() ^ (sizeof(SortedGeom) << 40)), CVQ_ERR_STATE,
                 "libcvq objects built from different headers (rebuild all)");
-    CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 512 (2-D) / 255 (3-D)");
+    CVQ_REQUIRE(S.n <= sorted_max_n(S.dim), CVQ_ERR_UNSUPPORTED, "SORTED supports n <= 1024 (2-D) / 255 (3-D)");
+    CVQ_REQUIRE(!(sweep && S.n > sorted_max_n_nt(S.dim, kSortNT)), CVQ_ERR_UNSUPPORTED, "SWEEP supports n <= 512");
     const SortedLaunch L{S, P, G, T, stream, a, tA, tB, pi, mode, bounds, out, snaps, hdr, fused, stamps, sweep};
-    const int nt = sorted_threads(T, S.dim);
+    const int nt = sorted_threads(T, S.dim, S.n);
     switch (nt) {
         case 1024: sorted_slice_1024(L); break;
         case 512: sorted_slice_512(L); break;

@@ -212,8 +212,14 @@ __device__ __forceinline__ void unpack_node(uint32_t c, int ns, int* a0, int* i1
 // double2 is 16-B aligned.  16-B records keep a node at 32 B of LDS reads (2-D):
 // the node loop is LDS-bandwidth bound, so wider records cost more than the VALU
 // work they save (measured).
-// largest n the kernel's register tables hold: the plan's 512 in 2-D, the 8-bit packing's 255 in 3-D
-__host__ __device__ constexpr int sorted_max_n(int dim) { return dim == 2 ? 512 : 255; }
+// largest n the kernel's register tables hold: 1024 in 2-D (the 16-bit LDS byte offsets of kLay2
+// reach 16 (2 ns - 1) < 2^16), the 8-bit packing's 255 in 3-D.  Per width: the 256- to 512-thread
+// 2-D instances hold n <= 512 (one or two grid indices per thread); n > 512 runs the 1024-thread
+// instance (sorted_threads), so the others keep their register budget
+__host__ __device__ constexpr int sorted_max_n(int dim) { return dim == 2 ? 1024 : 255; }
+__host__ __device__ constexpr int sorted_max_n_nt(int dim, int nt) {
+    return dim == 2 ? (nt >= 1024 ? 1024 : 512) : 255;
+}
 inline int sorted_stride(int n) { return (n + 1) & ~1; }
 // doubles of the table region
 __host__ __device__ inline int sorted_region_doubles(int layout, int n) {
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     __syncthreads();
     // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
     // axes unrolled so their latencies overlap; kept in registers until the path is chosen
-    constexpr int RPT = (sorted_max_n(DIM) + NT - 1) / NT;       // grid indices per thread
+    constexpr int RPT = (sorted_max_n_nt(DIM, NT) + NT - 1) / NT;   // grid indices per thread
     constexpr int ILP = sorted_ilp(COP, PM, DIM, NT);              // range sums' nodes in flight
     const int q = MSM ? S.q : 1;
     const double* fb = MSM ? a + t * DIM * q : nullptr;     // forecasts_by_states[t] (DIM, q)

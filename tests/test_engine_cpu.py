@@ -10,8 +10,11 @@ def test_auto_strategy_rules():
     for m in ("garch", "mean_reverting"):
         assert auto_strategy(m, 2, 64) == "sorted"
         assert auto_strategy(m, 2, 512) == "sorted"
-        with pytest.raises(ValueError, match="512"):
-            auto_strategy(m, 2, 513)                        # no plan takes n > 512: fail at the rule
+        assert auto_strategy(m, 2, 513) == "sorted"         # 512 < n <= 1024: SORTED's 1024-thread dates
+        assert auto_strategy(m, 2, 1024) == "sorted"
+        with pytest.raises(ValueError, match="1024"):
+            auto_strategy(m, 2, 1025)                       # no plan takes n > 1024: fail at the rule
+    assert auto_strategy("msm", 2, 1000, "student", [6.0, 0.5]) == "sorted"
     assert auto_strategy("msm", 3, 128) == "sorted"
     assert auto_strategy("garch", 3, 255) == "sorted"
     assert auto_strategy("msm", 2) == "compact"            # n unknown: the 2-D rule

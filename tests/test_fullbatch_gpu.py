@@ -3,12 +3,13 @@
 calc_var couples every date of a batch: the bisection runs max-over-dates iterations
 (Q2, calc_var_class.py:278) and stops every date at the first all-zero iteration (Q4,
 :293).  tests/golden/fullbatch_cfg{2,5,3}.npz hold the oracle's calc_var over the whole
-1000- / 5000-date batch of configs 2, 5 and 3 (inputs from the oracle's host forecast
-stage; tests/golden/gen_fullbatch.py).  Here the HIP solve of the same full batch must
+1000- / 5000-date batch of configs 2, 5 and 3, fullbatch_cfg4.npz over the first 250 of cfg 4's
+2000 dates (3 assets, 128^3, MSM k = 6; inputs from the oracle's host forecast stage;
+tests/golden/gen_fullbatch.py).  Here the HIP solve of the same full batch must
 give the same VaR vector bit for bit and the same global iteration count -- on one plan,
 and split into 2 and 4 contiguous date blocks (plans) joined by the packed finalize
 (cvq_solve_finalize_packed, the single all-gather's layout).  The strategy
-is auto (COMPACT for cfg 2 / 5, SORTED for cfg 3); cfg 5 also runs SORTED."""
+is auto (COMPACT for cfg 2 / 5, SORTED for cfg 3 / 4); cfg 5 also runs SORTED."""
 import os
 
 import numpy as np
@@ -19,7 +20,7 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-CASES = [(2, "auto"), (5, "auto"), (5, "sorted"), (3, "auto")]
+CASES = [(2, "auto"), (5, "auto"), (5, "sorted"), (3, "auto"), (4, "auto")]
 
 
 @pytest.fixture(scope="module", autouse=True)

@@ -99,13 +99,17 @@ def test_fullbatch_fixtures_are_consistent():
     from conftest import GOLDEN
     from copula_var import synthetic
     from oracle import forecast as F
-    for cfg, T in ((2, 1000), (5, 5000), (3, 5000)):
+    for cfg, T in ((2, 1000), (5, 5000), (3, 5000), (4, 250)):
         path = os.path.join(GOLDEN, f"fullbatch_cfg{cfg}.npz")
         z = dict(np.load(path, allow_pickle=False))
         assert int(z["T"]) == T and z["var"].shape == (T,) and not np.isnan(z["var"]).any()
         assert 19 <= int(z["iterations"]) <= 22 and not bool(z["broke"])
         c = synthetic.baseline_configs()[cfg]
-        _, ptf, windows = F.insample_split(synthetic.simulate_returns(c)[:c.n_in + 4], c.n_in, c.weights)
+        rets = synthetic.simulate_returns(c)
+        # the stored returns (the e2e GPU test's input) are the BASELINE batch's, cut to T dates
+        np.testing.assert_array_equal(z["returns"], rets[: c.n_in + T])
+        assert int(z["n_in"]) == c.n_in
+        _, ptf, windows = F.insample_split(rets[:c.n_in + 4], c.n_in, c.weights)
         assert ptf == float(z["ptf_mean"])
         if c.model == "msm":
             m = F.msm_integration_params(windows, c.msm_params, c.k, c.num_points)
