@@ -109,14 +109,17 @@ def test_fullbatch_fixtures_are_consistent():
         # the stored returns (the e2e GPU test's input) are the BASELINE batch's, cut to T dates
         np.testing.assert_array_equal(z["returns"], rets[: c.n_in + T])
         assert int(z["n_in"]) == c.n_in
-        _, ptf, windows = F.insample_split(rets[:c.n_in + 4], c.n_in, c.weights)
+        # first dates' windows (cfg 4, k = 6: all of its 250, as generated -- the batched filter's
+        # 64-state matmuls round differently per batch shape)
+        m4 = T if cfg == 4 else 4
+        _, ptf, windows = F.insample_split(rets[:c.n_in + m4], c.n_in, c.weights)
         assert ptf == float(z["ptf_mean"])
         if c.model == "msm":
             m = F.msm_integration_params(windows, c.msm_params, c.k, c.num_points)
-            np.testing.assert_array_equal(m["forecasts_by_states"], z["forecasts_by_states"][:4])
+            np.testing.assert_array_equal(m["forecasts_by_states"], z["forecasts_by_states"][:m4])
         else:
             np.testing.assert_array_equal(F.sigma_forecasts(windows, c.model, c.model_params()),
-                                          z["sigma_forecasts"][:4])
+                                          z["sigma_forecasts"][:m4])
 
 
 def test_q4_zero_case_oracle():
