@@ -736,7 +736,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // whose row lengths run from 0 to ~n, so the owner of row r sums the first half
     // of row r and the second half of row n - 1 - r (long rows pair with short ones)
     // sl: the slab's host schedule (0 = (lower, fg], 1 = (sg0, fg], 2 = (fg, sg1]; -1: none)
-    auto fixed_slab = [&](double va, double vb, int sl) {
+    // this thread's part of the slab (va, vb] (fixed_part) and the workgroup sum (fixed_slab -> sums[0])
+    auto fixed_part = [&](double va, double vb, int sl) -> double {
         double part = 0.0;
         if (G.fpair && sl >= 0) {
             auto cut = [&](const int16_t* c, double v) {
@@ -758,8 +759,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
                     nev += max(j1 - j0 + 1, 0);
                 }
             }
-            sums[0] = team_sum1<NT>(part, red, parity);
-            return;
+            return part;
         }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
@@ -778,17 +778,42 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             if (b2 > m2) part += range_sum(r2, m2 + 1, b2);
             nev += max(m1 - a1, 0) + max(b2 - m2, 0);
         }
-        sums[0] = team_sum1<NT>(part, red, parity);
+        return part;
     };
+    auto fixed_slab = [&](double va, double vb, int sl) { sums[0] = team_sum1<NT>(fixed_part(va, vb, sl), red, parity); };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    fixed_slab(P.lower, P.fg, 0);
-    const double r0 = sums[0];
+    // speculation (P.spec): while few dates of the plan's solves had r0 >= obj, the second slab's
+    // usual candidate (fg, sg1] is summed beside r0 and both reduced at once -- one workgroup
+    // reduction and one dependent phase fewer; each value comes from the same schedule and the same
+    // reduction order as alone, so the VaR is bit-identical with or without it
+    bool spec = false;
+    if (P.spec != nullptr && G.fpair != nullptr) {
+        const unsigned long long hi_cnt = __hip_atomic_load(&P.spec[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long all_cnt = __hip_atomic_load(&P.spec[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spec = 8 * hi_cnt <= all_cnt;
+    }
+    double r0, nr_spec = 0.0;
+    if (spec) {
+        double p0 = fixed_part(P.lower, P.fg, 0), p2 = fixed_part(P.fg, P.sg1, 2);
+        double s3[3];
+        team_sum3<NT>(p0, p2, 0.0, red, parity, s3);
+        r0 = s3[0];
+        nr_spec = s3[1];
+    } else {
+        fixed_slab(P.lower, P.fg, 0);
+        r0 = sums[0];
+    }
     stamp(2);
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    fixed_slab(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1);
+    if (P.spec != nullptr && tid == 0) {
+        if (r0 >= P.obj) atomicAdd(&P.spec[0], 1ull);
+        atomicAdd(&P.spec[1], 1ull);
+    }
+    if (spec && nl == P.fg && nu == P.sg1) sums[0] = nr_spec;
+    else fixed_slab(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1);
     const double nr = sums[0];
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);

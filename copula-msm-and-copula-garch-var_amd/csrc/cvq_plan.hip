@@ -904,7 +904,11 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
                             tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
                             {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]},
                             (tab && p->kcut_ok) ? p->d_kcut : nullptr, fpair_sched ? p->d_fpair : nullptr};
-        return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
+        // CVQ_SPEC=0: never speculate the second slab (A/B)
+        static const bool spec_on = !(getenv("CVQ_SPEC") && atoi(getenv("CVQ_SPEC")) == 0);
+        SolveConst Pc = P;
+        Pc.spec = spec_on ? (unsigned long long*)(p->d_err + 4) : nullptr;
+        return launch_compact(p->S, Pc, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
@@ -1086,6 +1090,7 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.fin_var = nullptr;
     P.fin_err = nullptr;
     P.exact_walk = dyadic_walk_ok(a, K) ? 1 : 0;
+    P.spec = nullptr;
     return P;
 }
 
@@ -1283,13 +1288,13 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if ((rc = dev_alloc(&p->d_kmax, kmax.size()))) break;
         if ((rc = dev_alloc(&p->d_off, off.size()))) break;
         if ((rc = dev_alloc(&p->d_hdr, 1))) break;
-        if ((rc = dev_alloc(&p->d_err, 4))) break;
+        if ((rc = dev_alloc(&p->d_err, 8))) break;   // [4] error words + ticket, [4..7] COMPACT's spec counters
     } while (0);
     if (rc) { cvq_plan_destroy(p); return rc; }
     hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     p->stream = p->own_stream;
-    e = hipMemset(p->d_err, 0, 4 * sizeof(int));         // error words + the fused-finalize ticket
+    e = hipMemset(p->d_err, 0, 8 * sizeof(int));         // error words + the fused-finalize ticket + spec counters
     if (e == hipSuccess) e = hipMemset(p->d_hdr, 0, sizeof(Header));
     if (e == hipSuccess) e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
