@@ -787,12 +787,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // usual candidate (fg, sg1] is summed beside r0 and both reduced at once -- one workgroup
     // reduction and one dependent phase fewer; each value comes from the same schedule and the same
     // reduction order as alone, so the VaR is bit-identical with or without it
-    bool spec = false;
-    if (P.spec != nullptr && G.fpair != nullptr) {
-        const unsigned long long hi_cnt = __hip_atomic_load(&P.spec[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long all_cnt = __hip_atomic_load(&P.spec[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spec = 8 * hi_cnt <= all_cnt;
-    }
+    const bool spec = P.spec != nullptr && G.fpair != nullptr && *P.spec != 0;
     double r0, nr_spec = 0.0;
     if (spec) {
         double p0 = fixed_part(P.lower, P.fg, 0), p2 = fixed_part(P.fg, P.sg1, 2);
@@ -808,10 +803,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
     const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    if (P.spec != nullptr && tid == 0) {
-        if (r0 >= P.obj) atomicAdd(&P.spec[0], 1ull);
-        atomicAdd(&P.spec[1], 1ull);
-    }
+    if (P.spec != nullptr && tid == 0) P.spec_flag[t] = r0 >= P.obj ? 1 : 0;   // the next solve's policy
     if (spec && nl == P.fg && nu == P.sg1) sums[0] = nr_spec;
     else fixed_slab(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1);
     const double nr = sums[0];
@@ -1093,6 +1085,21 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     return false;
 }
 
+// The speculation policy of the plan's next solve (SolveConst::spec), by the finalizing workgroup:
+// speculate while at most one date in eight needed the second slab (sg0, fg].
+template <int NT>
+__device__ __forceinline__ void spec_policy(const SolveConst& P, long long T) {
+    if (P.spec == nullptr) return;
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    int c = 0;
+    for (long long d = threadIdx.x; d < T; d += NT) c += P.spec_flag[d];
+    if (c) atomicAdd(&cnt, c);
+    __syncthreads();
+    if (threadIdx.x == 0) *P.spec = 8LL * cnt <= T ? 1 : 0;
+}
+
 // The solve over T dates: GEN = false, one workgroup per date (grid T); GEN = true, a
 // small grid working through the dates the fast kernel deferred (none: every workgroup
 // leaves at once).  Fused finalize (P.fin_var) by the last workgroup of the launch that
@@ -1118,6 +1125,7 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         __threadfence();
         if (!defer || __hip_atomic_load(&defer[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
             fused_finalize<NT>(P, hdr, snaps, T);
+            spec_policy<NT>(P, T);
         } else if (tid == 0) {
             P.fin_err[3] = 0;                            // the generic kernel finalizes
         }
@@ -1135,7 +1143,10 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         __syncthreads();
         if (!last) return;
         __threadfence();
-        if (cnt > 0 && P.fin_var) fused_finalize<NT>(P, hdr, snaps, T);
+        if (cnt > 0 && P.fin_var) {
+            fused_finalize<NT>(P, hdr, snaps, T);
+            spec_policy<NT>(P, T);
+        }
         __syncthreads();
         if (tid == 0) {
             defer[0] = 0;                                // reset for the next solve

@@ -168,6 +168,7 @@ struct cvq_plan {
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
     int* d_fpair = nullptr;      // [3][NT RPT] COMPACT fixed slabs' half-row pairs per thread slot
+    unsigned char* d_specflag = nullptr;   // [capDefer - 2] COMPACT: r0 >= obj per date (speculation policy)
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -895,6 +896,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         if (p->capDefer < p->T + 2) {                      // zeroed once; the generic kernel resets it
             if ((rc = dev_alloc(&p->d_defer, (size_t)p->T + 2))) return rc;
             CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
+            if ((rc = dev_alloc(&p->d_specflag, (size_t)p->T))) return rc;
             p->capDefer = p->T + 2;
         }
         const bool tab = p->ccount_depth >= 0;
@@ -907,7 +909,8 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         // CVQ_SPEC=0: never speculate the second slab (A/B)
         static const bool spec_on = !(getenv("CVQ_SPEC") && atoi(getenv("CVQ_SPEC")) == 0);
         SolveConst Pc = P;
-        Pc.spec = spec_on ? (unsigned long long*)(p->d_err + 4) : nullptr;
+        Pc.spec = spec_on ? p->d_err + 4 : nullptr;
+        Pc.spec_flag = spec_on ? p->d_specflag : nullptr;
         return launch_compact(p->S, Pc, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
@@ -1091,6 +1094,7 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.fin_err = nullptr;
     P.exact_walk = dyadic_walk_ok(a, K) ? 1 : 0;
     P.spec = nullptr;
+    P.spec_flag = nullptr;
     return P;
 }
 
@@ -1288,13 +1292,14 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if ((rc = dev_alloc(&p->d_kmax, kmax.size()))) break;
         if ((rc = dev_alloc(&p->d_off, off.size()))) break;
         if ((rc = dev_alloc(&p->d_hdr, 1))) break;
-        if ((rc = dev_alloc(&p->d_err, 8))) break;   // [4] error words + ticket, [4..7] COMPACT's spec counters
+        if ((rc = dev_alloc(&p->d_err, 8))) break;   // [4] error words + ticket, [4] COMPACT's speculation word
     } while (0);
     if (rc) { cvq_plan_destroy(p); return rc; }
     hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     p->stream = p->own_stream;
-    e = hipMemset(p->d_err, 0, 8 * sizeof(int));         // error words + the fused-finalize ticket + spec counters
+    e = hipMemset(p->d_err, 0, 8 * sizeof(int));         // error words + the fused-finalize ticket
+    if (e == hipSuccess) e = hipMemset(p->d_err + 4, 1, 1);   // speculation word: 1 (on) until a solve says otherwise
     if (e == hipSuccess) e = hipMemset(p->d_hdr, 0, sizeof(Header));
     if (e == hipSuccess) e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
@@ -1385,7 +1390,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_fpair, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_fpair, (void*)p->d_specflag, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_pass,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
