@@ -736,7 +736,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // whose row lengths run from 0 to ~n, so the owner of row r sums the first half
     // of row r and the second half of row n - 1 - r (long rows pair with short ones)
     // sl: the slab's host schedule (0 = (lower, fg], 1 = (sg0, fg], 2 = (fg, sg1]; -1: none)
-    // this thread's part of the slab (va, vb] (fixed_part) and the workgroup sum (fixed_slab -> sums[0])
+    // this thread's part of the slab (va, vb]
     auto fixed_part = [&](double va, double vb, int sl) -> double {
         double part = 0.0;
         if (G.fpair && sl >= 0) {
@@ -780,7 +780,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         }
         return part;
     };
-    auto fixed_slab = [&](double va, double vb, int sl) { sums[0] = team_sum1<NT>(fixed_part(va, vb, sl), red, parity); };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
     // speculation (P.spec): while few dates of the plan's solves had r0 >= obj, the second slab's
@@ -788,25 +787,35 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     // reduction and one dependent phase fewer; each value comes from the same schedule and the same
     // reduction order as alone, so the VaR is bit-identical with or without it
     const bool spec = P.spec != nullptr && G.fpair != nullptr && *P.spec != 0;
-    double r0, nr_spec = 0.0;
-    if (spec) {
-        double p0 = fixed_part(P.lower, P.fg, 0), p2 = fixed_part(P.fg, P.sg1, 2);
+    // both phases run through ONE copy of the fixed-slab code (a loop, not unrolled): the kernel's
+    // instruction footprint is what the CU's instruction cache holds while its dates sit at
+    // different phases
+    double r0 = 0.0, nr = 0.0, nl = P.fg, nu = P.fg;
+    double fva[2] = {P.lower, P.fg}, fvb[2] = {P.fg, P.sg1};
+    int fsl[2] = {0, 2}, fcnt = spec ? 2 : 1;
+#pragma nounroll
+    for (int ph = 0; ph < 2; ++ph) {
+        double fp[2] = {0.0, 0.0};
+#pragma nounroll
+        for (int e = 0; e < fcnt; ++e) {
+            const double x = fixed_part(e == 0 ? fva[0] : fva[1], e == 0 ? fvb[0] : fvb[1], e == 0 ? fsl[0] : fsl[1]);
+            if (e == 0) fp[0] = x; else fp[1] = x;
+        }
         double s3[3];
-        team_sum3<NT>(p0, p2, 0.0, red, parity, s3);
+        team_sum3<NT>(fp[0], fp[1], 0.0, red, parity, s3);
+        if (ph == 1) { nr = s3[0]; break; }
         r0 = s3[0];
-        nr_spec = s3[1];
-    } else {
-        fixed_slab(P.lower, P.fg, 0);
-        r0 = sums[0];
+        stamp(2);
+        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+        nu = (r0 < P.obj) ? P.sg1 : P.fg;
+        if (P.spec != nullptr && tid == 0) P.spec_flag[t] = r0 >= P.obj ? 1 : 0;   // the next solve's policy
+        if (spec && nl == P.fg && nu == P.sg1) { nr = s3[1]; break; }
+        fva[0] = nl;
+        fvb[0] = nu;
+        fsl[0] = (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1;
+        fcnt = 1;
     }
-    stamp(2);
-    const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-    const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
-    if (P.spec != nullptr && tid == 0) P.spec_flag[t] = r0 >= P.obj ? 1 : 0;   // the next solve's policy
-    if (spec && nl == P.fg && nu == P.sg1) sums[0] = nr_spec;
-    else fixed_slab(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1);
-    const double nr = sums[0];
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);
     double lo = __builtin_nan(""), hi = __builtin_nan("");
