@@ -168,7 +168,7 @@ struct cvq_plan {
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
     int* d_fpair = nullptr;      // [3][NT RPT] COMPACT fixed slabs' half-row pairs per thread slot
-    unsigned char* d_specflag = nullptr;   // [capDefer - 2] COMPACT: r0 >= obj per date (speculation policy)
+    unsigned char* d_specflag = nullptr;   // COMPACT speculation: policy word [0], r0 >= obj per date from [256]
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -896,7 +896,10 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         if (p->capDefer < p->T + 2) {                      // zeroed once; the generic kernel resets it
             if ((rc = dev_alloc(&p->d_defer, (size_t)p->T + 2))) return rc;
             CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
-            if ((rc = dev_alloc(&p->d_specflag, (size_t)p->T))) return rc;
+            // speculation word at [0] (its own 256-B line, away from the ticket's atomics), flags from [256]
+            if ((rc = dev_alloc(&p->d_specflag, (size_t)p->T + 256))) return rc;
+            CVQ_HIP_CHECK(hipMemsetAsync(p->d_specflag, 0, 256, p->stream));
+            CVQ_HIP_CHECK(hipMemsetAsync(p->d_specflag, 1, 1, p->stream));   // 1: speculate until a solve says otherwise
             p->capDefer = p->T + 2;
         }
         const bool tab = p->ccount_depth >= 0;
@@ -909,8 +912,8 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         // CVQ_SPEC=0: never speculate the second slab (A/B)
         static const bool spec_on = !(getenv("CVQ_SPEC") && atoi(getenv("CVQ_SPEC")) == 0);
         SolveConst Pc = P;
-        Pc.spec = spec_on ? p->d_err + 4 : nullptr;
-        Pc.spec_flag = spec_on ? p->d_specflag : nullptr;
+        Pc.spec = spec_on ? (int*)p->d_specflag : nullptr;
+        Pc.spec_flag = spec_on ? p->d_specflag + 256 : nullptr;
         return launch_compact(p->S, Pc, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
@@ -1292,14 +1295,13 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
         if ((rc = dev_alloc(&p->d_kmax, kmax.size()))) break;
         if ((rc = dev_alloc(&p->d_off, off.size()))) break;
         if ((rc = dev_alloc(&p->d_hdr, 1))) break;
-        if ((rc = dev_alloc(&p->d_err, 8))) break;   // [4] error words + ticket, [4] COMPACT's speculation word
+        if ((rc = dev_alloc(&p->d_err, 4))) break;
     } while (0);
     if (rc) { cvq_plan_destroy(p); return rc; }
     hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate failed"); cvq_plan_destroy(p); return CVQ_ERR_HIP; }
     p->stream = p->own_stream;
-    e = hipMemset(p->d_err, 0, 8 * sizeof(int));         // error words + the fused-finalize ticket
-    if (e == hipSuccess) e = hipMemset(p->d_err + 4, 1, 1);   // speculation word: 1 (on) until a solve says otherwise
+    e = hipMemset(p->d_err, 0, 4 * sizeof(int));         // error words + the fused-finalize ticket
     if (e == hipSuccess) e = hipMemset(p->d_hdr, 0, sizeof(Header));
     if (e == hipSuccess) e = hipMemcpy(p->d_x, x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_F, F.data(), F.size() * sizeof(double), hipMemcpyHostToDevice);
