@@ -59,12 +59,6 @@ struct SolveConst {
     int* fin_err;                 // [4]: error, kstop, N, workgroup ticket (0 between launches)
     int exact_walk;               // every bracket's bisection points are exact dyadics (dyadic_walk_ok):
                                   // COMPACT's tail walks its remaining levels in closed form, one per lane
-    // COMPACT speculation: while few dates need the second slab (sg0, fg] (r0 >= obj), the solve sums
-    // the usual candidate (fg, sg1] beside r0 in one reduction -- a schedule only: the values are
-    // bit-identical either way.  spec[0]: 1 = speculate, written by the last workgroup of the previous
-    // fused solve from spec_flag[T] (per date: r0 >= obj); nullptr: never.
-    int* spec;
-    unsigned char* spec_flag;
 };
 
 struct alignas(16) Header {       // per-rank solve summary, all-gathered across ranks

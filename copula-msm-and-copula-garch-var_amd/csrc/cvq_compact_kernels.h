@@ -782,40 +782,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     };
 
     // ---- (i)-(iii): calc_var_class.py:114-160 (Q1, Q3)
-    // speculation (P.spec): while few dates of the plan's solves had r0 >= obj, the second slab's
-    // usual candidate (fg, sg1] is summed beside r0 and both reduced at once -- one workgroup
-    // reduction and one dependent phase fewer; each value comes from the same schedule and the same
-    // reduction order as alone, so the VaR is bit-identical with or without it
-    const bool spec = P.spec != nullptr && G.fpair != nullptr && *P.spec != 0;
-    // both phases run through ONE copy of the fixed-slab code (a loop, not unrolled): the kernel's
-    // instruction footprint is what the CU's instruction cache holds while its dates sit at
-    // different phases
-    double r0 = 0.0, nr = 0.0, nl = P.fg, nu = P.fg;
-    double fva[2] = {P.lower, P.fg}, fvb[2] = {P.fg, P.sg1};
-    int fsl[2] = {0, 2}, fcnt = spec ? 2 : 1;
-#pragma nounroll
-    for (int ph = 0; ph < 2; ++ph) {
-        double fp[2] = {0.0, 0.0};
-#pragma nounroll
-        for (int e = 0; e < fcnt; ++e) {
-            const double x = fixed_part(e == 0 ? fva[0] : fva[1], e == 0 ? fvb[0] : fvb[1], e == 0 ? fsl[0] : fsl[1]);
-            if (e == 0) fp[0] = x; else fp[1] = x;
-        }
-        double s3[3];
-        team_sum3<NT>(fp[0], fp[1], 0.0, red, parity, s3);
-        if (ph == 1) { nr = s3[0]; break; }
-        r0 = s3[0];
-        stamp(2);
-        nl = (r0 >= P.obj) ? P.sg0 : P.fg;
-        nu = (r0 < P.obj) ? P.sg1 : P.fg;
-        if (P.spec != nullptr && tid == 0) P.spec_flag[t] = r0 >= P.obj ? 1 : 0;   // the next solve's policy
-        if (spec && nl == P.fg && nu == P.sg1) { nr = s3[1]; break; }
-        fva[0] = nl;
-        fvb[0] = nu;
-        fsl[0] = (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1;
-        fcnt = 1;
-    }
+    const double r0 = team_sum1<NT>(fixed_part(P.lower, P.fg, 0), red, parity);
+    stamp(2);
+    const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
+    const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
     const double prevU0 = (nl == P.sg0) ? P.sg0 : P.fg;
+    const double nr = team_sum1<NT>(fixed_part(nl, nu, (nl == P.sg0 && nu == P.fg) ? 1 : (nl == P.fg && nu == P.sg1) ? 2 : -1),
+                                    red, parity);
     const double F = (nl == P.fg) ? r0 + nr : r0 - nr;
     stamp(3);
     double lo = __builtin_nan(""), hi = __builtin_nan("");
@@ -1094,21 +1067,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     return false;
 }
 
-// The speculation policy of the plan's next solve (SolveConst::spec), by the finalizing workgroup:
-// speculate while at most one date in eight needed the second slab (sg0, fg].
-template <int NT>
-__device__ __forceinline__ void spec_policy(const SolveConst& P, long long T) {
-    if (P.spec == nullptr) return;
-    __shared__ int cnt;
-    if (threadIdx.x == 0) cnt = 0;
-    __syncthreads();
-    int c = 0;
-    for (long long d = threadIdx.x; d < T; d += NT) c += P.spec_flag[d];
-    if (c) atomicAdd(&cnt, c);
-    __syncthreads();
-    if (threadIdx.x == 0) *P.spec = 8LL * cnt <= T ? 1 : 0;
-}
-
 // The solve over T dates: GEN = false, one workgroup per date (grid T); GEN = true, a
 // small grid working through the dates the fast kernel deferred (none: every workgroup
 // leaves at once).  Fused finalize (P.fin_var) by the last workgroup of the launch that
@@ -1134,7 +1092,6 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         __threadfence();
         if (!defer || __hip_atomic_load(&defer[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
             fused_finalize<NT>(P, hdr, snaps, T);
-            spec_policy<NT>(P, T);
         } else if (tid == 0) {
             P.fin_err[3] = 0;                            // the generic kernel finalizes
         }
@@ -1152,10 +1109,7 @@ __global__ CVQ_COMPACT_BOUNDS(NT) void k_compact(StaticDev S, SolveConst P, Comp
         __syncthreads();
         if (!last) return;
         __threadfence();
-        if (cnt > 0 && P.fin_var) {
-            fused_finalize<NT>(P, hdr, snaps, T);
-            spec_policy<NT>(P, T);
-        }
+        if (cnt > 0 && P.fin_var) fused_finalize<NT>(P, hdr, snaps, T);
         __syncthreads();
         if (tid == 0) {
             defer[0] = 0;                                // reset for the next solve

@@ -168,7 +168,6 @@ struct cvq_plan {
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
     int* d_fpair = nullptr;      // [3][NT RPT] COMPACT fixed slabs' half-row pairs per thread slot
-    unsigned char* d_specflag = nullptr;   // COMPACT speculation: policy word [0], r0 >= obj per date from [256]
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -896,10 +895,6 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
         if (p->capDefer < p->T + 2) {                      // zeroed once; the generic kernel resets it
             if ((rc = dev_alloc(&p->d_defer, (size_t)p->T + 2))) return rc;
             CVQ_HIP_CHECK(hipMemsetAsync(p->d_defer, 0, ((size_t)p->T + 2) * sizeof(int), p->stream));
-            // speculation word at [0] (its own 256-B line, away from the ticket's atomics), flags from [256]
-            if ((rc = dev_alloc(&p->d_specflag, (size_t)p->T + 256))) return rc;
-            CVQ_HIP_CHECK(hipMemsetAsync(p->d_specflag, 0, 256, p->stream));
-            CVQ_HIP_CHECK(hipMemsetAsync(p->d_specflag, 1, 1, p->stream));   // 1: speculate until a solve says otherwise
             p->capDefer = p->T + 2;
         }
         const bool tab = p->ccount_depth >= 0;
@@ -909,12 +904,7 @@ int launch_solve(cvq_plan* p, const SolveConst& P, double* snaps, Header* hdr) {
                             tab ? p->d_ccount : nullptr, p->ccount_depth, p->d_tlist, p->d_tvs,
                             {p->bstart[0], p->bstart[1], p->bstart[2], p->bstart[3]},
                             (tab && p->kcut_ok) ? p->d_kcut : nullptr, fpair_sched ? p->d_fpair : nullptr};
-        // CVQ_SPEC=0: never speculate the second slab (A/B)
-        static const bool spec_on = !(getenv("CVQ_SPEC") && atoi(getenv("CVQ_SPEC")) == 0);
-        SolveConst Pc = P;
-        Pc.spec = spec_on ? (int*)p->d_specflag : nullptr;
-        Pc.spec_flag = spec_on ? p->d_specflag + 256 : nullptr;
-        return launch_compact(p->S, Pc, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
+        return launch_compact(p->S, P, G, p->T, p->stream, p->in_a, p->d_tA, p->d_tB, p->in_pi, direct_fused(p), st,
                               snaps, hdr, p->d_defer, !p->fast_hint, kernel_abi_key() ^ (sizeof(CompactGeom) << 40));
     }
     if (p->strategy != CVQ_STRATEGY_PREFIX) {
@@ -1096,8 +1086,6 @@ SolveConst solve_const(const cvq_solve_args& a, int K) {
     P.fin_var = nullptr;
     P.fin_err = nullptr;
     P.exact_walk = dyadic_walk_ok(a, K) ? 1 : 0;
-    P.spec = nullptr;
-    P.spec_flag = nullptr;
     return P;
 }
 
@@ -1392,7 +1380,7 @@ int32_t cvq_plan_destroy(cvq_plan* p) {
     for (void* b : {(void*)p->d_x, (void*)p->d_F, (void*)p->d_phi, (void*)p->d_uvs, (void*)p->d_cf, (void*)p->d_kmax,
                     (void*)p->d_off, (void*)p->d_a, (void*)p->d_pi, (void*)p->d_tA, (void*)p->d_tB,
                     (void*)p->d_C, (void*)p->d_snap, (void*)p->d_hdr, (void*)p->d_err, (void*)p->d_io, (void*)p->d_stamps,
-                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_fpair, (void*)p->d_specflag, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
+                    (void*)p->d_cutfix, (void*)p->d_kcut, (void*)p->d_fpair, (void*)p->d_ccount, (void*)p->d_tlist, (void*)p->d_tvs, (void*)p->d_defer, (void*)p->d_vstar, (void*)p->d_bucket, (void*)p->d_sidx, (void*)p->d_svs,
                     (void*)p->d_tree, (void*)p->d_pass,
                     (void*)p->d_pidx, (void*)p->d_pvs})
         if (b) (void)hipFree(b);
