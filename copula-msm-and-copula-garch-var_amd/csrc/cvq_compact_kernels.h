@@ -94,9 +94,6 @@ enum { kCutLower = 0, kCutSg0, kCutFg, kCutSg1, kCutVmin, kCutVmax };
 #define CVQ_BLK_PER_THREAD 12
 #endif
 constexpr int kBlkPerThread = CVQ_BLK_PER_THREAD;
-#ifndef CVQ_TAIL_COND
-#define CVQ_TAIL_COND 0
-#endif
 // tail list word: row (bits 0-10) | column (bits 11-21) | last node of a tie group (bit 31)
 constexpr uint32_t kTlRowMask = 0x7FFu;
 constexpr int kTlColShift = 11;
@@ -915,14 +912,10 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         constexpr int NPT = kBlkPerThread;
         const int cnt = max(nbr_next, 0);
         const uint32_t* tl = G.tlist + ps;
-        // every word loaded and every node evaluated unconditionally (the list carries NT * NPT zero
-        // words past its end; word 0 is the valid node (0, 0)), the entries past the cell selected
-        // away: the NPT nodes' LDS reads and arithmetic interleave instead of one branch each
         uint32_t wd[NPT];
         double pre[NPT];                                          // local inclusive prefix
         double run = 0.0;
         nev += min(max(cnt - tid * NPT, 0), NPT);
-#if CVQ_TAIL_COND                                                 // A/B: one branch per node
 #pragma unroll
         for (int m = 0; m < NPT; ++m) wd[m] = (tid * NPT + m < cnt) ? tl[tid * NPT + m] : 0u;
 #pragma unroll
@@ -932,17 +925,6 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
             run += v;
             pre[m] = run;
         }
-#else
-#pragma unroll
-        for (int m = 0; m < NPT; ++m) wd[m] = tl[tid * NPT + m];
-#pragma unroll
-        for (int m = 0; m < NPT; ++m) {
-            const int r = (int)(wd[m] & kTlRowMask), j = (int)((wd[m] >> kTlColShift) & kTlRowMask);
-            const double v = node1(r, j);
-            run += (tid * NPT + m < cnt) ? v : 0.0;
-            pre[m] = run;
-        }
-#endif
         // block exclusive scan of the thread totals (one barrier)
         const double incl = wave_incl_scan_f64(run);
         double* wt = red + parity * (3 * (NT / 64));

@@ -1348,7 +1348,6 @@ int32_t cvq_plan_create(const cvq_static* s, int32_t device, cvq_plan** out) {
             const bool gend = i + 1 == ord.size() || !(vs[ord[i + 1]] == vs[ord[i]]);
             tl[i] = r | (j << kTlColShift) | (gend ? kTlGroupEnd : 0u);
         }
-        tl.resize(tl.size() + compact_tail_cap(), 0u);   // the block tail loads a full cell's words past the end
         if ((rc = dev_alloc(&p->d_tlist, tl.size())) || (rc = dev_alloc(&p->d_tvs, p->hvc.size()))) {
             cvq_plan_destroy(p);
             return rc;
