@@ -238,6 +238,7 @@ def main():
         t0 = time.perf_counter()
         for i in range(steps):
             step_fn(i % n_batches)
+        t_enq = time.perf_counter() - t0                  # host time to enqueue the K steps
         if bracket is not None:
             ev1.record(streams[0])
         torch.cuda.synchronize()
@@ -256,8 +257,10 @@ def main():
             kt[kind] = (sum(m for m, _ in ms_n), sum(n_ for _, n_ in ms_n))
         for k in range(n_batches):       # convergence within the bisection budget (outside the timed region)
             plans[k].solve_status()
+        enq_ms.append(t_enq / steps * 1e3)
         return el, kt
 
+    enq_ms = []                                       # host enqueue time per step of each timed leg
     dom = "mass" if a.strategy == "prefix" else "solve"                      # dominant kernel
     # no HIP events between the timed legs' launches (an event record between two launches on
     # a stream delays the second: rocprofv3 saw ~10 us gaps in an event-timed one-batch leg)
@@ -384,6 +387,7 @@ def main():
                        "global_dates": T_total, "n_in": c.n_in, "parallelism": f"dates/dp{world}",
                        "strategy": a.strategy, "inflight": nf},
             "single_solve": single,
+            "host_enqueue_ms_per_step": enq_ms[0] if enq_ms else None,
             "roofline": {"bound": "hbm" if hbm_bound else "fp64-valu",
                          "achieved": pmc_gbs if hbm_bound else fp64_tflops,
                          "peak": HBM_PEAK_GBS if hbm_bound else FP64_PEAK_TFLOPS,

@@ -48,6 +48,13 @@ __host__ __device__ __forceinline__ double inner_coord(const StaticDev& S, doubl
     return inner_coord_div(v - lev, S.w0);
 }
 
+// Element idx of a global table through a 32-bit byte offset: the load takes the SGPR-base +
+// VGPR-offset form (no 64-bit address arithmetic per load).  Tables below 4 GB only.
+template <class T>
+__device__ __forceinline__ T ld32(const T* __restrict__ base, unsigned idx) {
+    return *(const T*)((const char*)base + idx * (unsigned)sizeof(T));
+}
+
 struct SolveConst {
     double obj, fg, sg0, sg1, vmin, vmax, lower, tol;
     int K;                        // bisection iterations executed (>= reference's count)

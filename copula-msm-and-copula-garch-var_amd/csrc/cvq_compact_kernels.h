@@ -572,7 +572,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int k = 0; k < RPT; ++k)
-            krt[b][k] = (G.kcut && G.ccount) ? G.kcut[(((size_t)b << G.cdepth) + 1) * n + min(tid + NT * k, n - 1)] : 0;
+            krt[b][k] = (G.kcut && G.ccount) ? ld32(G.kcut, (unsigned)((((b << G.cdepth) + 1) * n) + min(tid + NT * k, n - 1))) : 0;
 
     // ---- tables: index i -> row record i (axis 0) and column record i (axis 1)
     const int q = MSM ? S.q : 1;
@@ -594,8 +594,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
                     const int bb = min(b, q - 1);
                     wa[b] = fb[bb];
                     wb[b] = fb[q + bb];
-                    fr[b] = S.F[(size_t)bb * n + i];
-                    fc[b] = S.F[((size_t)q + bb) * n + i];
+                    fr[b] = ld32(S.F, (unsigned)(bb * n + i));
+                    fc[b] = ld32(S.F, (unsigned)((q + bb) * n + i));
                 }
                 // states b >= q: weight 0 (F finite: fma(0, F, w) == w), so no load waits
                 // behind a branch on b < q
@@ -606,13 +606,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
                 }
             } else {
                 for (int b = 0; b < q; ++b) {
-                    wr = fma(fb[b], S.F[(size_t)b * n + i], wr);
-                    wc = fma(fb[q + b], S.F[((size_t)q + b) * n + i], wc);
+                    wr = fma(fb[b], ld32(S.F, (unsigned)(b * n + i)), wr);
+                    wc = fma(fb[q + b], ld32(S.F, (unsigned)((q + b) * n + i)), wc);
                 }
             }
         } else {
             wr = S.F[i];
-            wc = S.F[(size_t)n + i];
+            wc = ld32(S.F, (unsigned)(n + i));
         }
         // GARCH / UKF Student: a dead entry (z = +-inf or NaN: u in {0, 1}) zeroes its nodes in the
         // reference (k_sorted's table phase, student.py:130-131, :166-167, nan_to_num): record
@@ -846,8 +846,8 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int rr = own[k] ? row[k] : 0;
-            kml[k] = tnext ? kc0[(size_t)(2 * hc) * n + rr] : 0;
-            kmh[k] = tnext ? kc0[(size_t)(2 * hc + 1) * n + rr] : 0;
+            kml[k] = tnext ? ld32(kc0, (unsigned)(2 * hc * n + rr)) : 0;
+            kmh[k] = tnext ? ld32(kc0, (unsigned)((2 * hc + 1) * n + rr)) : 0;
         }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {

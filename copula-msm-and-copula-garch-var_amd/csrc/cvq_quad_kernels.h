@@ -77,7 +77,9 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
                                            double* u_out, double* pdf_out) {
     if (MSM) {
         const double* f = a + td * S.q;
-        const double* ph = S.phi + (size_t)d * S.q * S.n + i;
+        // 32-bit element offsets into the static table (dim q n <= 12288 entries): the loads take
+        // the SGPR base + VGPR offset form, no 64-bit address arithmetic per load
+        const unsigned ph0 = (unsigned)(d * S.q * S.n + i);
         double acc;
         if (S.q <= kQUnroll) {                                   // every load issued before the sum
             // the weights of states s >= q are 0 (their Phi loads repeat state q - 1's finite
@@ -87,13 +89,13 @@ __device__ __forceinline__ void marginal_u(const StaticDev& S, const double* __r
 #pragma unroll
             for (int s = 0; s < kQUnroll; ++s) fv[s] = f[min(s, S.q - 1)];
 #pragma unroll
-            for (int s = 0; s < kQUnroll; ++s) pv[s] = ph[(size_t)min(s, S.q - 1) * S.n];
+            for (int s = 0; s < kQUnroll; ++s) pv[s] = ld32(S.phi, ph0 + (unsigned)(min(s, S.q - 1) * S.n));
             acc = fv[0] * pv[0];
 #pragma unroll
             for (int s = 1; s < kQUnroll; ++s) acc = acc + (s < S.q ? fv[s] : 0.0) * pv[s];
         } else {
-            acc = f[0] * ph[0];
-            for (int s = 1; s < S.q; ++s) acc += f[s] * ph[(size_t)s * S.n];
+            acc = f[0] * ld32(S.phi, ph0);
+            for (int s = 1; s < S.q; ++s) acc += f[s] * ld32(S.phi, ph0 + (unsigned)(s * S.n));
         }
         *u_out = acc;                                            // msm_integration_function.py:34-36
         *pdf_out = 1.0;
