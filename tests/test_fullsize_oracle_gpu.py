@@ -240,15 +240,27 @@ def test_slabs_ending_at_zero(case, strategy):
 
 @pytest.mark.parametrize("strategy", ["auto", "compact", "sorted", "direct", "prefix"])
 def test_2d_grid_above_512_refused_at_creation(strategy):
-    """num_points > 512 is refused when the plan is created, for every strategy (ADVICE r03
-    feared an 'auto' plan that builds and then fails every solve)."""
+    """2-D num_points in (512, 1024] runs on SORTED only (r06; auto picks it): every other strategy
+    refuses it when the plan is created, and every strategy refuses n > 1024 there (ADVICE r03
+    feared an 'auto' plan that builds and then fails every solve).  The SORTED solves at n = 700 /
+    1024 are checked against the oracle in tests/test_large_grid_gpu.py."""
     from copula_var import synthetic, tables
-    c = synthetic.baseline_configs()[1].with_(T=4, num_points=600)
-    rets = synthetic.simulate_returns(c)
-    _, ptf, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
-    ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
-    with pytest.raises(ValueError, match="512"):
-        _plan(c, ipt, uvs, ggp, strategy=strategy)
+    for n, ok in ((600, strategy in ("auto", "sorted")), (1025, False)):
+        c = synthetic.baseline_configs()[1].with_(T=4, num_points=n)
+        rets = synthetic.simulate_returns(c)
+        _, ptf, centred, _ = tables.insample_split(rets, c.n_in, c.weights)
+        ipt, uvs, ggp = tables.sigma_integration_params(centred, c.n_in, c.model, c.model_params(), c.num_points)
+        if ok:
+            p = _plan(c, ipt, uvs, ggp, strategy=strategy)
+            try:
+                assert p.strategy == "sorted"
+                var, it = p.calc_var(ptf)
+                assert np.all(np.isfinite(var))
+            finally:
+                p.close()
+        else:
+            with pytest.raises(ValueError, match="512|1024"):
+                _plan(c, ipt, uvs, ggp, strategy=strategy)
 
 
 @pytest.mark.parametrize("case", ["cfg1", "cfg4_k4_n16"])
