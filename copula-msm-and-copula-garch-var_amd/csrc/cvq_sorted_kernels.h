@@ -57,6 +57,9 @@ constexpr int kSortBlk = CVQ_SORT_BLK;
 #ifndef CVQ_SORT_ILP
 #define CVQ_SORT_ILP 4
 #endif
+#ifndef CVQ_SORT_SPLIT
+#define CVQ_SORT_SPLIT 1           // 3-D: r0 split at sg0, the second slab (sg0, fg] from the same reduction
+#endif
 #ifndef CVQ_SORT_SKIP
 #define CVQ_SORT_SKIP 1            // range sums skip the partial rounds' slots past the range
 #endif
@@ -231,7 +234,7 @@ inline size_t sorted_lds_bytes(int n, int nt, int dim, bool sweep = false, int l
     if (layout < 0) layout = sorted_layout(dim, n);
     // SWEEP: wave-total slots [NT / 64] + per boundary its prefix value, position and children
     const size_t sw = sweep ? sizeof(double) * ((size_t)nt / 64 + kPassMax) + sizeof(int) * 2 * kPassMax : 0;
-    return sizeof(double) * ((size_t)sorted_region_doubles(layout, n) + 2 * (nt / 64) + kSortScalars) +
+    return sizeof(double) * ((size_t)sorted_region_doubles(layout, n) + 4 * (nt / 64) + kSortScalars) +
            sizeof(double2) * sorted_tail_cap(dim) + sw;
 }
 
@@ -294,11 +297,11 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     constexpr int FG = LAY == kLay3F ? 4 : 1;      // fg1 stride
     double* fr2 = LAY == kLay3F ? lds + kLay3FAx2 / 8 : fg1 + (DIM == 3 ? 1 : 0) * ns;   // fast [ns][2] inner axis
     double2* tail = (double2*)(lds + sorted_region_doubles(LAY, n));   // [TCAP] (v*, value)
-    double* red = (double*)(tail + TCAP);          // [2][NT / 64] reduction slots
-    int& flags = *(int*)(red + 2 * (NT / 64));     // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
-    double& s_arest = *(red + 2 * (NT / 64) + 1);  // 3-D: the axis-0 weight off the plane i1 == 0
-    int& last = *(int*)(red + 2 * (NT / 64) + 2);  // fused finalize: this workgroup is the last
-    double* sred = red + 2 * (NT / 64) + kSortScalars;   // SWEEP: [NT / 64] wave totals
+    double* red = (double*)(tail + TCAP);          // [2 parity][2 values][NT / 64] reduction slots
+    int& flags = *(int*)(red + 4 * (NT / 64));     // bit 0: non-finite or zero table entry, bit 1: pi not rank 1
+    double& s_arest = *(red + 4 * (NT / 64) + 1);  // 3-D: the axis-0 weight off the plane i1 == 0
+    int& last = *(int*)(red + 4 * (NT / 64) + 2);  // fused finalize: this workgroup is the last
+    double* sred = red + 4 * (NT / 64) + kSortScalars;   // SWEEP: [NT / 64] wave totals
     double* Pvs = sred + NT / 64;                  // SWEEP: [kPassMax] prefix values (pass A, then B)
     int* Bls = (int*)(Pvs + kPassMax);             // SWEEP: [kPassMax] boundary positions
     int* Chs = Bls + kPassMax;                     // SWEEP: [kPassMax] packed child boundaries
@@ -638,7 +641,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     auto team_sum = [&](double v) {                        // workgroup sum, identical in every thread; one barrier
         v = wave_sum(v);
         if constexpr (NT == 64) return v;
-        double* rr = red + parity * (NT / 64);
+        double* rr = red + parity * (2 * (NT / 64));
         parity ^= 1;
         if (lane == 0) rr[tid >> 6] = v;
         __syncthreads();
@@ -646,6 +649,24 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) s0 += rr[w];
         return s0;
+    };
+    auto team_sum2 = [&](double v0, double v1, double& s0, double& s1) {   // two sums, one barrier
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        double* rr = red + parity * (2 * (NT / 64));
+        parity ^= 1;
+        if (lane == 0) {
+            rr[tid >> 6] = v0;
+            rr[NT / 64 + (tid >> 6)] = v1;
+        }
+        __syncthreads();
+        s0 = rr[0];
+        s1 = rr[NT / 64];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w) {
+            s0 += rr[w];
+            s1 += rr[NT / 64 + w];
+        }
     };
 
     if (mode == 1) {                                       // compute_integral of bounds[t]
@@ -830,14 +851,31 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
       }
     }
     if (!passed) {
-        const double r0 = team_sum(range_sum(G.fix[0], G.fix[2]));   // (lower, fg]
+        // 3-D: r0 = I(lower, fg] as (lower, sg0] + (sg0, fg] when the positions are ordered -- the
+        // second slab (sg0, fg] of the dates with r0 >= obj (cfg 4: 99.6% of its dates, VaR below -3.5)
+        // then comes from the same pass and reduction instead of being evaluated a second time.  Not
+        // in 2-D: the BASELINE 2-D workloads' dates have r0 < obj, and the extra live sum costs the
+        // Plackett instances an occupancy step (75 -> 81 VGPRs)
+        const bool split = CVQ_SORT_SPLIT && DIM == 3 && G.fix[0] <= G.fix[1] && G.fix[1] <= G.fix[2];
+        double r0, n2 = 0.0;
+        if (split) {
+            const double p2 = range_sum(G.fix[1], G.fix[2]);
+            team_sum2(range_sum(G.fix[0], G.fix[1]) + p2, p2, r0, n2);
+        } else {
+            r0 = team_sum(range_sum(G.fix[0], G.fix[2]));           // (lower, fg]
+        }
         stamp(2);
         nodes += max(G.fix[2] - G.fix[0], 0);
         const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
         const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
-        const double nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+        double nr;
+        if (split && nl == P.sg0 && nu == P.fg) {
+            nr = n2;
+        } else {
+            nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
+            nodes += max(fixpos(nu) - fixpos(nl), 0);
+        }
         stamp(3);
-        nodes += max(fixpos(nu) - fixpos(nl), 0);
         bracket(r0, nl, nu, nr);
     }
     // the remaining levels above the tails: one range sum + one workgroup reduction each
