@@ -121,10 +121,10 @@ struct CompactGeom {
     // with ccount: [4][2^cdepth][n] per-row cuts cnt_r(mid) of every bisection cell the levels split
     // (heap nodes 1 .. 2^cdepth - 1; date-independent, host-built); nullptr: the levels search the grid
     const int16_t* kcut;
-    // [3][NT RPT] the fixed slabs' schedule: slot tid + NT k sums two half-rows of slab (lower, fg],
-    // (sg0, fg] or (fg, sg1], int16 codes 2 r + h (h = 1: the second half of row r; -1: none) in the
-    // low / high half-word, host-paired longest with shortest (ensure_cutfix); nullptr: slot k of
-    // thread tid takes the first half of row r and the second half of row n - 1 - r
+    // [3][NT RPT][2] the fixed slabs' schedule: slot tid + NT k sums two half-rows of slab (lower, fg],
+    // (sg0, fg] or (fg, sg1], each given as its column range row | j0 << 10 | len << 20 (0: none),
+    // host-paired longest with shortest (ensure_cutfix); nullptr: slot k of thread tid takes the
+    // first half of row r and the second half of row n - 1 - r
     const int* fpair;
 };
 
@@ -560,12 +560,13 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int w = min(tid + NT * k, (kCutLds / 2) * n - 1);
         cv[k] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
     }
-    // the fixed slabs' half-row pairs (host schedule G.fpair): (lower, fg], (sg0, fg], (fg, sg1]
-    int fpv[3][RPT];
+    // the fixed slabs' half-row column ranges (host schedule G.fpair): (lower, fg], (sg0, fg], (fg, sg1]
+    int2 fpv[3][RPT];
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
-        for (int k = 0; k < RPT; ++k) fpv[s3][k] = G.fpair ? G.fpair[s3 * NT * RPT + tid + NT * k] : 0;
+        for (int k = 0; k < RPT; ++k)
+            fpv[s3][k] = G.fpair ? ((const int2*)G.fpair)[s3 * NT * RPT + tid + NT * k] : make_int2(0, 0);
     // the first bisection level's per-row cuts of all four brackets (host table G.kcut, heap node 1)
     int krt[4][RPT];
 #pragma unroll
@@ -740,23 +741,17 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     auto fixed_part = [&](double va, double vb, int sl) -> double {
         double part = 0.0;
         if (G.fpair && sl >= 0) {
-            auto cut = [&](const int16_t* c, double v) {
-                return v == P.lower ? c[kCutLower] : v == P.sg0 ? c[kCutSg0] : v == P.fg ? c[kCutFg]
-                     : v == P.sg1 ? c[kCutSg1] : v == P.vmin ? c[kCutVmin] : c[kCutVmax];
-            };
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
-                const int w = sl == 0 ? fpv[0][k] : sl == 1 ? fpv[1][k] : fpv[2][k];
+                const int2 w2 = sl == 0 ? fpv[0][k] : sl == 1 ? fpv[1][k] : fpv[2][k];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-                    const int code = (int)(int16_t)(e == 0 ? (w & 0xFFFF) : ((unsigned)w >> 16));
-                    if (code < 0) continue;
-                    const int r = code >> 1;
-                    const int16_t* c = cfx + (size_t)r * kCutLds;
-                    const int a = cut(c, va), b = max((int)cut(c, vb), a), m = a + (b - a + 1) / 2;
-                    const int j0 = (code & 1) ? m + 1 : a + 1, j1 = (code & 1) ? b : m;
-                    if (j1 >= j0) part += range_sum(r, j0, j1);
-                    nev += max(j1 - j0 + 1, 0);
+                    const unsigned w = (unsigned)(e == 0 ? w2.x : w2.y);
+                    const int len = (int)(w >> 20);
+                    if (len == 0) continue;
+                    const int j0 = (int)__builtin_amdgcn_ubfe(w, 10, 10);
+                    part += range_sum((int)(w & 0x3FFu), j0, j0 + len - 1);
+                    nev += len;
                 }
             }
             return part;

@@ -167,7 +167,7 @@ struct cvq_plan {
     int bstart[4] = {0, 0, 0, 0};   // ub(bracket lower) in hvc for the cached solve arguments
     int* d_defer = nullptr;      // [2 + T]: generic-path dates deferred by the fast kernel (count, ticket, list)
     int16_t* d_kcut = nullptr;   // [4][2^ccount_depth][n] per-row cuts of the bisection cells' mids
-    int* d_fpair = nullptr;      // [3][NT RPT] COMPACT fixed slabs' half-row pairs per thread slot
+    int* d_fpair = nullptr;      // [3][NT RPT][2] COMPACT fixed slabs' half-row column ranges per thread slot
     bool kcut_ok = false;
     long long capDefer = 0;
     bool fast_hint = false;      // every date of the batch takes COMPACT's fast path (proven or asserted)
@@ -722,26 +722,29 @@ int ensure_cutfix(cvq_plan* p, const SolveConst& P) {
     // shortest, a wave's lanes carry similar work (the fixed slabs are triangles and corner bands:
     // row lengths run from 0 to ~n, and the loops run to the wave's longest lane); any assignment
     // that takes every half-row once gives the same slab, so this is a schedule, not a semantics.
+    // Each half-row goes to the kernel as its column range: row | j0 << 10 | len << 20 (len 0: none).
     {
         const int NT = compact_nt(), M = NT * ((n + NT - 1) / NT);
-        std::vector<int> fp((size_t)3 * M);
+        std::vector<int> fp((size_t)3 * M * 2);
         const int cols[3][2] = {{kCutLower, kCutFg}, {kCutSg0, kCutFg}, {kCutFg, kCutSg1}};
-        std::vector<std::pair<int, int>> hl((size_t)2 * M);
+        struct Half { int len, r, j0; };
+        std::vector<Half> hl((size_t)2 * M);
         for (int sl = 0; sl < 3; ++sl) {
             for (int r = 0; r < n; ++r) {
                 const int a = h[(size_t)r * kCutFixed + cols[sl][0]];
                 const int b = std::max<int>(h[(size_t)r * kCutFixed + cols[sl][1]], a);
                 const int m = a + (b - a + 1) / 2;
-                hl[2 * r] = {m - a, 2 * r};                  // first half (a, m]
-                hl[2 * r + 1] = {b - m, 2 * r + 1};          // second half (m, b]
+                hl[2 * r] = {m - a, r, a + 1};               // first half: columns (a, m]
+                hl[2 * r + 1] = {b - m, r, m + 1};           // second half: (m, b]
             }
-            for (int e = 2 * n; e < 2 * M; ++e) hl[e] = {-1, -1};   // no half-row
-            std::stable_sort(hl.begin(), hl.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
-                return x.first > y.first;
-            });
+            for (int e = 2 * n; e < 2 * M; ++e) hl[e] = {0, 0, 0};
+            std::stable_sort(hl.begin(), hl.end(), [](const Half& x, const Half& y) { return x.len > y.len; });
+            auto word = [](const Half& x) {
+                return x.len > 0 ? (int)((uint32_t)x.r | ((uint32_t)x.j0 << 10) | ((uint32_t)x.len << 20)) : 0;
+            };
             for (int e = 0; e < M; ++e) {
-                const int ca = hl[e].second, cb = hl[2 * M - 1 - e].second;
-                fp[(size_t)sl * M + e] = (int)((uint32_t)(ca & 0xFFFF) | ((uint32_t)(cb & 0xFFFF) << 16));
+                fp[((size_t)sl * M + e) * 2] = word(hl[e]);
+                fp[((size_t)sl * M + e) * 2 + 1] = word(hl[2 * M - 1 - e]);
             }
         }
         if (!p->d_fpair && (rc0 = dev_alloc(&p->d_fpair, fp.size()))) return rc0;
