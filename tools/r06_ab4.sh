@@ -1,5 +1,6 @@
 #!/bin/bash
 # cfg 4 A/B of the SORTED r0 split (build_variants/nosplit: CVQ_SORT_SPLIT=0): full batch, 250 dates, e2e;
+# cfg 2 / 5 A/B of the COMPACT fixed-slab column ranges (build_variants/halfrow: the half-row codes);
 # the cfg 4 full-batch parity tests first
 set -uo pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -19,5 +20,9 @@ for rep in 1 2; do
   for args in "--config 4 --steps 20 --warmup 3" "--config 4 --steps 50 --warmup 5 --dates-per-gpu 250 --inflight 1 --e2e 0"; do
     run main $main "$args" || exit 1
     run nosplit $GRAFT_REPO_ROOT/build_variants/nosplit/libcvq.so "$args" || exit 1
+  done
+  for args in "--steps 100 --warmup 5 --e2e 0" "--config 5 --steps 50 --warmup 5 --e2e 0"; do
+    run main $main "$args" || exit 1
+    run halfrow $GRAFT_REPO_ROOT/build_variants/halfrow/libcvq.so "$args" || exit 1
   done
 done
