@@ -26,3 +26,9 @@ for rep in 1 2; do
     run halfrow $GRAFT_REPO_ROOT/build_variants/halfrow/libcvq.so "$args" || exit 1
   done
 done
+# the 20-step window: 20 steps with 5 and with 50 warmup steps, and 100 steps
+for rep in 1 2; do
+  run s20w5 $main "--steps 20 --warmup 5 --e2e 0" || exit 1
+  run s20w50 $main "--steps 20 --warmup 50 --e2e 0" || exit 1
+  run s100w5 $main "--steps 100 --warmup 5 --e2e 0" || exit 1
+done
