@@ -561,12 +561,16 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         cv[k] = ((const int*)G.cutfix)[(w / (kCutLds / 2)) * (kCutFixed / 2) + w % (kCutLds / 2)];
     }
     // the fixed slabs' half-row column ranges (host schedule G.fpair): (lower, fg], (sg0, fg], (fg, sg1]
-    int2 fpv[3][RPT];
+    // (plain ints, selected with compile-time indices: an int2 array selected by slab went to scratch)
+    int fpx[3][RPT], fpy[3][RPT];
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
-        for (int k = 0; k < RPT; ++k)
-            fpv[s3][k] = G.fpair ? ((const int2*)G.fpair)[s3 * NT * RPT + tid + NT * k] : make_int2(0, 0);
+        for (int k = 0; k < RPT; ++k) {
+            const int2 w2 = G.fpair ? ((const int2*)G.fpair)[s3 * NT * RPT + tid + NT * k] : make_int2(0, 0);
+            fpx[s3][k] = w2.x;
+            fpy[s3][k] = w2.y;
+        }
     // the first bisection level's per-row cuts of all four brackets (host table G.kcut, heap node 1)
     int krt[4][RPT];
 #pragma unroll
@@ -743,10 +747,11 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         if (G.fpair && sl >= 0) {
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
-                const int2 w2 = sl == 0 ? fpv[0][k] : sl == 1 ? fpv[1][k] : fpv[2][k];
+                const int wx = sl == 0 ? fpx[0][k] : sl == 1 ? fpx[1][k] : fpx[2][k];
+                const int wy = sl == 0 ? fpy[0][k] : sl == 1 ? fpy[1][k] : fpy[2][k];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-                    const unsigned w = (unsigned)(e == 0 ? w2.x : w2.y);
+                    const unsigned w = (unsigned)(e == 0 ? wx : wy);
                     const int len = (int)(w >> 20);
                     if (len == 0) continue;
                     const int j0 = (int)__builtin_amdgcn_ubfe(w, 10, 10);
