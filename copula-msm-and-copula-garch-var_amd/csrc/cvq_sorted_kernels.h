@@ -60,6 +60,9 @@ constexpr int kSortBlk = CVQ_SORT_BLK;
 #ifndef CVQ_SORT_SPLIT
 #define CVQ_SORT_SPLIT 1           // 3-D: r0 split at sg0, the second slab (sg0, fg] from the same reduction
 #endif
+#ifndef CVQ_SORT_SPEC2
+#define CVQ_SORT_SPEC2 1           // 2-D: (fg, sg1] reduced beside r0
+#endif
 #ifndef CVQ_SORT_SKIP
 #define CVQ_SORT_SKIP 1            // range sums skip the partial rounds' slots past the range
 #endif
@@ -857,19 +860,26 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         // in 2-D: the BASELINE 2-D workloads' dates have r0 < obj, and the extra live sum costs the
         // Plackett instances an occupancy step (75 -> 81 VGPRs)
         const bool split = CVQ_SORT_SPLIT && DIM == 3 && G.fix[0] <= G.fix[1] && G.fix[1] <= G.fix[2];
+        // 2-D: the second slab's usual candidate (fg, sg1] (every BASELINE 2-D date has r0 < obj) is
+        // summed beside r0 and reduced with it -- one phase and barrier fewer on the date's chain; the
+        // same range sums and reduction order as alone, so the values are bit-identical
+        const bool spec2 = CVQ_SORT_SPEC2 && DIM == 2 && G.fix[2] <= G.fix[3];
         double r0, n2 = 0.0;
         if (split) {
             const double p2 = range_sum(G.fix[1], G.fix[2]);
             team_sum2(range_sum(G.fix[0], G.fix[1]) + p2, p2, r0, n2);
+        } else if (spec2) {
+            const double p0 = range_sum(G.fix[0], G.fix[2]);
+            team_sum2(p0, range_sum(G.fix[2], G.fix[3]), r0, n2);
         } else {
             r0 = team_sum(range_sum(G.fix[0], G.fix[2]));           // (lower, fg]
         }
         stamp(2);
-        nodes += max(G.fix[2] - G.fix[0], 0);
+        nodes += max(G.fix[2] - G.fix[0], 0) + (spec2 ? max(G.fix[3] - G.fix[2], 0) : 0);
         const double nl = (r0 >= P.obj) ? P.sg0 : P.fg;
         const double nu = (r0 < P.obj) ? P.sg1 : P.fg;
         double nr;
-        if (split && nl == P.sg0 && nu == P.fg) {
+        if ((split && nl == P.sg0 && nu == P.fg) || (spec2 && nl == P.fg && nu == P.sg1)) {
             nr = n2;
         } else {
             nr = team_sum(range_sum(fixpos(nl), fixpos(nu)));
