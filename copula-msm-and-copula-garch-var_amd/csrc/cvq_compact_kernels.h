@@ -901,7 +901,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     }
 
     // ---- block tail (host cell tables): the cell (lo, hi] = sorted positions [ps, ps + cnt).
-    // Thread tid evaluates positions tid * kb + m in order; a block scan turns the values
+    // Thread tid evaluates positions tid * NPT + m in order; a block scan turns the values
     // into F at every node threshold (F = prev + prefix when the last level moved lo, else
     // prev - (cell total - prefix): the reference's adjust_integral chain after its first
     // level).  F is non-decreasing in v (node values >= 0; a NaN makes every later F NaN),
@@ -911,21 +911,17 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
     if (tabc && it < P.K) {
         constexpr int NPT = kBlkPerThread;
         const int cnt = max(nbr_next, 0);
-        // positions per thread: the cell spread over the whole workgroup (kb <= NPT, uniform), so a
-        // cell well below NT * NPT nodes takes kb sequential node steps instead of NPT
-        const int kb = min(NPT, max((cnt + NT - 1) / NT, 1));
-        const int e0 = tid * kb;
         const uint32_t* tl = G.tlist + ps;
         uint32_t wd[NPT];
         double pre[NPT];                                          // local inclusive prefix
         double run = 0.0;
-        nev += min(max(cnt - e0, 0), kb);
+        nev += min(max(cnt - tid * NPT, 0), NPT);
 #pragma unroll
-        for (int m = 0; m < NPT; ++m) wd[m] = (m < kb && e0 + m < cnt) ? tl[e0 + m] : 0u;
+        for (int m = 0; m < NPT; ++m) wd[m] = (tid * NPT + m < cnt) ? tl[tid * NPT + m] : 0u;
 #pragma unroll
         for (int m = 0; m < NPT; ++m) {
             const int r = (int)(wd[m] & kTlRowMask), j = (int)((wd[m] >> kTlColShift) & kTlRowMask);
-            const double v = (m < kb && e0 + m < cnt) ? node1(r, j) : 0.0;
+            const double v = (tid * NPT + m < cnt) ? node1(r, j) : 0.0;
             run += v;
             pre[m] = run;
         }
@@ -947,7 +943,7 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         int mc = NPT, ma = NPT, mz = NPT;
 #pragma unroll
         for (int m = NPT - 1; m >= 0; --m) {
-            if (!(wd[m] & kTlGroupEnd) || m >= kb || e0 + m >= cnt) continue;
+            if (!(wd[m] & kTlGroupEnd) || tid * NPT + m >= cnt) continue;
             const double pa = base + pre[m];
             const double Fv = ustack ? prev + pa : prev - (Stot - pa);
             if (!(Fv < P.obj)) mc = m;
@@ -966,9 +962,9 @@ __device__ __forceinline__ bool compact_date(const StaticDev& S, const SolveCons
         const int mcl = __shfl(mc, lc, 64), mal = __shfl(ma, la, 64), mzl = __shfl(mz, lz, 64);
         if (lane == 0) {
             int* e = ew + 4 * (tid >> 6);
-            e[0] = bc ? ((tid >> 6) * 64 + lc) * kb + mcl : kNoPos;
-            e[1] = ba ? ((tid >> 6) * 64 + la) * kb + mal : kNoPos;
-            e[2] = bz ? ((tid >> 6) * 64 + lz) * kb + mzl : kNoPos;
+            e[0] = bc ? ((tid >> 6) * 64 + lc) * NPT + mcl : kNoPos;
+            e[1] = ba ? ((tid >> 6) * 64 + la) * NPT + mal : kNoPos;
+            e[2] = bz ? ((tid >> 6) * 64 + lz) * NPT + mzl : kNoPos;
         }
         __syncthreads();
         stamp(29);

@@ -914,7 +914,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     }
 
     // ---- block tail: the cell (lo, hi] = v*-sorted positions [plo, phi), TCAP < phi - plo <= BCAP.
-    // Thread tid evaluates positions plo + tid * kb + m in order (kb <= kSortBlk); a block scan turns the
+    // Thread tid evaluates positions plo + tid * kSortBlk + m in order; a block scan turns the
     // values into F at every node threshold (F = prev + prefix when the last level moved lo, else
     // prev - (cell total - prefix): the reference's adjust_integral chain after its first level).
     // F is non-decreasing in v (node values >= 0; a NaN makes every later F NaN), so every
@@ -924,22 +924,19 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     if (blk_tail) {
         constexpr int KB = kSortBlk;
         const int cnt = phi - plo;
-        // positions per thread: the cell spread over the whole workgroup (kb <= KB, uniform), so a
-        // cell well below NT * KB nodes takes kb sequential node steps instead of KB
-        const int kb = min(KB, max((cnt + NT - 1) / NT, 1));
-        const int e0 = tid * kb;                           // my first cell entry
+        const int e0 = tid * KB;                           // my first cell entry
         uint32_t wd[KB];
         double vv[KB + 1];                                 // v* of my entries and of the next one
 #pragma unroll
-        for (int m = 0; m < KB; ++m) wd[m] = (m < kb && e0 + m < cnt) ? G.tidx[plo + e0 + m] : 0u;
+        for (int m = 0; m < KB; ++m) wd[m] = e0 + m < cnt ? G.tidx[plo + e0 + m] : 0u;
 #pragma unroll
-        for (int m = 0; m <= KB; ++m) vv[m] = (m <= kb && e0 + m < cnt) ? G.tvs[plo + e0 + m] : __builtin_inf();
+        for (int m = 0; m <= KB; ++m) vv[m] = e0 + m < cnt ? G.tvs[plo + e0 + m] : __builtin_inf();
         double pre[KB];                                    // my inclusive prefix
         double run = 0.0;
         auto eval_cell = [&](auto nodef) {
 #pragma unroll
             for (int m = 0; m < KB; ++m) {
-                const double v = (m < kb && e0 + m < cnt) ? nodef(wd[m]) : 0.0;
+                const double v = e0 + m < cnt ? nodef(wd[m]) : 0.0;
                 run += v;
                 pre[m] = run;
             }
@@ -964,7 +961,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         int mc = KB, ma = KB, mz = KB;
 #pragma unroll
         for (int m = KB - 1; m >= 0; --m) {
-            if (!(m < kb && e0 + m < cnt && vv[m + 1] > vv[m])) continue;   // tie-group ends only (inf past the cell)
+            if (!(e0 + m < cnt && vv[m + 1] > vv[m])) continue;   // tie-group ends only (inf past the cell)
             const double pa = base + pre[m];
             const double Fv = ustack ? prev + pa : prev - (Stot - pa);
             if (!(Fv < P.obj)) mc = m;
@@ -977,9 +974,9 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         const int mcl = __shfl(mc, lc, 64), mal = __shfl(ma, la, 64), mzl = __shfl(mz, lz, 64);
         if (lane == 0) {
             int* e = ew + 4 * (tid >> 6);
-            e[0] = bc ? ((tid >> 6) * 64 + lc) * kb + mcl : kNoPos;
-            e[1] = ba ? ((tid >> 6) * 64 + la) * kb + mal : kNoPos;
-            e[2] = bz ? ((tid >> 6) * 64 + lz) * kb + mzl : kNoPos;
+            e[0] = bc ? ((tid >> 6) * 64 + lc) * KB + mcl : kNoPos;
+            e[1] = ba ? ((tid >> 6) * 64 + la) * KB + mal : kNoPos;
+            e[2] = bz ? ((tid >> 6) * 64 + lz) * KB + mzl : kNoPos;
         }
         __syncthreads();
         stamp(29);
