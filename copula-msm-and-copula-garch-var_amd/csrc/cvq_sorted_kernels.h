@@ -328,19 +328,36 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     if (tid == 0) flags = 0;
     __syncthreads();
     // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
-    // axes unrolled so their latencies overlap; kept in registers until the path is chosen
+    // axes unrolled so their latencies overlap; kept in registers until the path is chosen.
+    // 2-D: thread tid holds indices tid + NT k of both axes.  3-D: the DIM n entries are spread
+    // flat over the workgroup (entry e = tid + NT k is axis e / n, index e mod n), so a wide
+    // workgroup's table phase is one entry deep instead of three (cfg 4 at 1024 threads: 384 of
+    // them busy instead of 128; a lone date's table phase is on its latency chain)
     constexpr int RPT = (sorted_max_n_nt(DIM, NT) + NT - 1) / NT;   // grid indices per thread
+    constexpr bool FLAT = DIM == 3;
+    constexpr int EPT = FLAT ? (DIM * sorted_max_n_nt(DIM, NT) + NT - 1) / NT : RPT * DIM;   // entries per thread
     constexpr int ILP = sorted_ilp(COP, PM, DIM, NT);              // range sums' nodes in flight
     const int q = MSM ? S.q : 1;
     const double* fb = MSM ? a + t * DIM * q : nullptr;     // forecasts_by_states[t] (DIM, q)
-    double eA[RPT][DIM], eB[RPT][DIM], eW[RPT][DIM];
+    double eA[EPT], eB[EPT], eW[EPT];
+    auto slot = [&](int sl, int& ax, int& i) -> bool {      // entry sl of this thread: (axis, index)
+        if constexpr (FLAT) {
+            const int e = tid + sl * NT;
+            ax = e / n;
+            i = e - ax * n;
+            return ax < DIM;
+        } else {
+            ax = sl % DIM;
+            i = tid + (sl / DIM) * NT;
+            return i < n;
+        }
+    };
     int bad = 0;
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        const int i = tid + k * NT;
-        if (i >= n) continue;
-#pragma unroll
-        for (int ax = 0; ax < DIM; ++ax) {
+    for (int sl = 0; sl < EPT; ++sl) {
+        int ax, i;
+        if (!slot(sl, ax, i)) continue;
+        {
             double A, B;
             if constexpr (FUSED) {
                 table_entry<COP, MSM, COP == CVQ_STUDENT, (COP == CVQ_STUDENT && PM == 6 + DIM) ? 6 : 0>(
@@ -363,9 +380,9 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
                 if (!(B * w > 0.0)) bad |= 1;              // fast records take logs of B w
                 if (!(fabs(A) < 1.0e15)) bad |= 1;         // fast powers / exps need a bounded quadratic form
             }
-            eA[k][ax] = A;
-            eB[k][ax] = B;
-            eW[k][ax] = w;
+            eA[sl] = A;
+            eB[sl] = B;
+            eW[sl] = w;
         }
     }
     const double* pit = pi + t * S.Q;
@@ -405,12 +422,11 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     const double k02 = DIM == 2 ? k01 : kq * (S.Ri[2] + S.Ri[6]);
     const double k12 = DIM == 3 ? kq * (S.Ri[5] + S.Ri[7]) : 0.0;
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int i = tid + k * NT;
-      if (i >= n) continue;
-#pragma unroll
-      for (int ax = 0; ax < DIM; ++ax) {
-        const double z = eA[k][ax], B = eB[k][ax], w = eW[k][ax];
+    for (int sl = 0; sl < EPT; ++sl) {
+      int ax, i;
+      if (!slot(sl, ax, i)) continue;
+      {
+        const double z = eA[sl], B = eB[sl], w = eW[sl];
         if (!fast) {
             zg[ax * n + i] = z;
             Bg[ax * n + i] = B;

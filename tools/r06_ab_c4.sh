@@ -1,0 +1,24 @@
+#!/bin/bash
+# cfg 4 A/B (in-tree library vs build_variants/<v>): full batch one at a time and in flight, 250 dates, e2e
+set -uo pipefail
+cd "$GRAFT_REPO_ROOT"
+tag=$1; v=$2
+out=gpurun_out/$tag
+mkdir -p $out
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_fullbatch_gpu.py \
+    tests/test_e2e_fullbatch_gpu.py tests/test_sorted_gpu.py > $out/pytest.txt 2>&1 || { tail -30 $out/pytest.txt; exit 1; }
+tail -1 $out/pytest.txt
+run() {
+  CVQ_LIB=$2 timeout -k 10 300 python3 bench.py $3 --other-configs none --cpu-baseline 0 > $out/b.json 2>$out/b.err \
+    || { echo "$1 failed"; tail -3 $out/b.err; return 1; }
+  python3 -c "
+import json; d=json.load(open('$out/b.json')); e=d.get('e2e') or {}; print('$1', '$3', round(d['value']/1e6,3), round(d['single_solve']['value']/1e6,3), round(d['roofline']['avg_launch_us'],2), round((e.get('value') or 0)/1e6,3), d['var_checksum'])" | tee -a $out/ab.txt
+}
+main=$GRAFT_REPO_ROOT/copula-msm-and-copula-garch-var_amd/copula_var/libcvq.so
+for rep in 1 2; do
+  for args in "--config 4 --steps 20 --warmup 3" "--config 4 --steps 50 --warmup 5 --dates-per-gpu 250 --inflight 1 --e2e 0" \
+              "--config 4 --steps 50 --warmup 5 --dates-per-gpu 500 --inflight 1 --e2e 0"; do
+    run main $main "$args" || exit 1
+    run $v $GRAFT_REPO_ROOT/build_variants/$v/libcvq.so "$args" || exit 1
+  done
+done
