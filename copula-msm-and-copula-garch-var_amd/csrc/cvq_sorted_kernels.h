@@ -129,6 +129,12 @@ struct SortedGeom {
 
 // exp_node: cvq_special.h (the fast records clamp their logs at kLogFloor, within its domain)
 constexpr double kLogFloor = -1.0e4;
+// the Gaussian node's exp: exp_node7 (4.0e-11 relative, two FMAs shorter) unless built with
+// CVQ_SORT_EXP7=0 (exp_node, 1.4e-14)
+#ifndef CVQ_SORT_EXP7
+#define CVQ_SORT_EXP7 1
+#endif
+__device__ __forceinline__ double exp_gauss(double x) { return CVQ_SORT_EXP7 ? exp_node7(x) : exp_node(x); }
 
 // b^-(m/2) for the fast path's b = 1 + z^T R^-1 z / nu: the fast path requires finite
 // |z| < 1e15 and R is positive definite, so 1 <= b < ~1e31 and b^(m/2) stays finite:
@@ -521,12 +527,12 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         const double2 C = rd2(rec2(c));
         if constexpr (COP == CVQ_GAUSSIAN) {
             if constexpr (DIM == 2) {
-                return exp_node(fma(A.x, C.x, A.y + C.y));
+                return exp_gauss(fma(A.x, C.x, A.y + C.y));
             } else {
                 const lds_f64* r1 = rec1(c);
                 const double2 Bv = rd2(r1);
                 const double g1 = LAY == kLay3F ? r1[2] : fg1[__builtin_amdgcn_ubfe(c, 9, 8)];
-                return exp_node(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
+                return exp_gauss(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
             }
         } else if constexpr (COP == CVQ_STUDENT) {
             double b, sc;
