@@ -129,12 +129,14 @@ struct SortedGeom {
 
 // exp_node: cvq_special.h (the fast records clamp their logs at kLogFloor, within its domain)
 constexpr double kLogFloor = -1.0e4;
-// the Gaussian node's exp: exp_node7 (4.0e-11 relative, two FMAs shorter) unless built with
-// CVQ_SORT_EXP7=0 (exp_node, 1.4e-14)
-#ifndef CVQ_SORT_EXP7
-#define CVQ_SORT_EXP7 1
+// the Gaussian node's exp: the records carry the exponent's terms scaled by log2(e), so the node is
+// 2^E' by exp2_node7 (4.0e-11 relative; no ln2 reduction: two FMAs and a multiply fewer than exp_node7,
+// four FMAs fewer than the degree-9 exp_node).  CVQ_SORT_EXP2=0: unscaled records and exp_node7.
+#ifndef CVQ_SORT_EXP2
+#define CVQ_SORT_EXP2 1
 #endif
-__device__ __forceinline__ double exp_gauss(double x) { return CVQ_SORT_EXP7 ? exp_node7(x) : exp_node(x); }
+constexpr double kGaussRecScale = CVQ_SORT_EXP2 ? 1.4426950408889634 : 1.0;   // log2(e)
+__device__ __forceinline__ double exp_gauss(double x) { return CVQ_SORT_EXP2 ? exp2_node7(x) : exp_node7(x); }
 
 // b^-(m/2) for the fast path's b = 1 + z^T R^-1 z / nu: the fast path requires finite
 // |z| < 1e15 and R is positive definite, so 1 <= b < ~1e31 and b^(m/2) stays finite:
@@ -427,6 +429,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     const double k01 = kq * (S.Ri[1] + S.Ri[DIM]);
     const double k02 = DIM == 2 ? k01 : kq * (S.Ri[2] + S.Ri[6]);
     const double k12 = DIM == 3 ? kq * (S.Ri[5] + S.Ri[7]) : 0.0;
+    const double g02 = kGaussRecScale * k02;                // the Gaussian 3-D node's (0, 2) cross term, scaled
 #pragma unroll
     for (int sl = 0; sl < EPT; ++sl) {
       int ax, i;
@@ -441,22 +444,24 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
         }
         const double kcc = kq * S.Ri[ax * (DIM + 1)] * (z * z);          // diagonal term of axis ax
         if constexpr (COP == CVQ_GAUSSIAN) {
-            // log factors g = log(B w) - Ri_cc z^2 / 2, clamped at kLogFloor; E = sum g + cross
+            // log factors g = log(B w) - Ri_cc z^2 / 2, clamped at kLogFloor; E = sum g + cross; every
+            // term that enters E scaled by kGaussRecScale (E' = E log2(e), the node 2^E')
+            constexpr double L = kGaussRecScale;
             auto lg = [](double v) { return fmax(log(v), kLogFloor); };
             if (ax == 0) {
-                fr0[2 * i] = DIM == 2 ? k02 * z : z;
-                fr0[2 * i + 1] = lg(S.term1 * B * (DIM == 3 ? arest : w)) + kcc;
+                fr0[2 * i] = DIM == 2 ? (L * k02) * z : z;
+                fr0[2 * i + 1] = L * (lg(S.term1 * B * (DIM == 3 ? arest : w)) + kcc);
                 if (DIM == 3) {                                              // plane i1 == 0 (Q6)
                     fr0[2 * (n + i)] = z;
-                    fr0[2 * (n + i) + 1] = lg(S.term1 * B * w) + kcc;
+                    fr0[2 * (n + i) + 1] = L * (lg(S.term1 * B * w) + kcc);
                 }
             } else if (ax == DIM - 1) {
                 fr2[2 * i] = z;
-                fr2[2 * i + 1] = lg(B * w) + kcc;
+                fr2[2 * i + 1] = L * (lg(B * w) + kcc);
             } else {
-                fr1[R1 * i] = k01 * z;
-                fr1[R1 * i + 1] = k12 * z;
-                fg1[FG * i] = lg(B * w) + kcc;
+                fr1[R1 * i] = (L * k01) * z;
+                fr1[R1 * i + 1] = (L * k12) * z;
+                fg1[FG * i] = L * (lg(B * w) + kcc);
             }
         } else if constexpr (COP == CVQ_PLACKETT) {       // rec0 = (-2 u, theta s), rec2 = ((theta - 1) v, s)
             double* r = ax == 0 ? fr0 + 2 * i : fr2 + 2 * i;
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
                 const lds_f64* r1 = rec1(c);
                 const double2 Bv = rd2(r1);
                 const double g1 = LAY == kLay3F ? r1[2] : fg1[__builtin_amdgcn_ubfe(c, 9, 8)];
-                return exp_gauss(fma(A.x, fma(k02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
+                return exp_gauss(fma(A.x, fma(g02, C.x, Bv.x), fma(Bv.y, C.x, (A.y + g1) + C.y)));
             }
         } else if constexpr (COP == CVQ_STUDENT) {
             double b, sc;

@@ -429,6 +429,23 @@ __device__ __forceinline__ double exp_node7(double x) {
     return __builtin_amdgcn_ldexp(p, (int)k);
 }
 
+// 2^x as exp_node7 in t = r / ln2 (coefficient k times ln2^k; tools/exp_fit.py --base2): k = rint(x),
+// t = x - k exact, no ln2 reduction -- for arguments already scaled by log2(e) (the SORTED Gaussian
+// records).  4.0e-11 relative; x < -1075 underflows to 0, NaN stays NaN; finite |x| < 1e9.
+__device__ __forceinline__ double exp2_node7(double x) {
+    const double k = __builtin_rint(x);
+    const double t = x - k;
+    double p = 1.5199910599689e-05;
+    p = fma(p, t, 0.000154692740464984);
+    p = fma(p, t, 0.001333393130124095);
+    p = fma(p, t, 0.009618027317530873);
+    p = fma(p, t, 0.055504103426500875);
+    p = fma(p, t, 0.24022651197562325);
+    p = fma(p, t, 0.6931471807317516);
+    p = fma(p, t, 0.9999999999617687);
+    return __builtin_amdgcn_ldexp(p, (int)k);
+}
+
 // log(b) for finite b > 0 (the node power base, the quantile tail pp): b = 2^k m, m in [sqrt(1/2), sqrt(2)),
 // log(1 + f) from s = f / (2 + f) and the published fdlibm e_log.c minimax polynomial in s^2
 // (< 1 ulp there; the reciprocal here is v_rcp_f64 + two Newton steps, ~1 ulp more), no

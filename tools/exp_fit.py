@@ -1,6 +1,7 @@
 """Fit exp's polynomial on |r| <= ln2/2 with (near-)equioscillating relative error (cvq_special.h
 exp_node7).  Weighted Chebyshev least squares, reweighted by the current error; prints the max
-relative error of the double Horner evaluation and the coefficients (r^0 first)."""
+relative error of the double Horner evaluation and the coefficients (r^0 first).  --base2: the same
+polynomial in t = r / ln2 (2^t on |t| <= 1/2, exp2_node7: coefficient k times ln2^k)."""
 import sys
 
 import numpy as np
@@ -21,8 +22,13 @@ def fit(deg, iters=30, n=4000):
 
 
 if __name__ == "__main__":
-    deg = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    deg = int(args[0]) if args else 7
     coef, err = fit(deg)
-    print(f"degree {deg}: max relative error {err:.3g}")
+    if "--base2" in sys.argv:
+        coef = [c * np.log(2) ** k for k, c in enumerate(coef)]
+        ts = np.linspace(-0.5, 0.5, 200001)
+        err = float(np.max(np.abs(P.polyval(ts, coef) / np.exp2(ts) - 1)))
+    print(f"degree {deg}{' (2^t)' if '--base2' in sys.argv else ''}: max relative error {err:.3g}")
     for k, v in enumerate(coef):
         print(k, repr(float(v)))
