@@ -142,13 +142,13 @@ __device__ __forceinline__ double exp_gauss(double x) { return CVQ_SORT_EXP2 ? e
 // |z| < 1e15 and R is positive definite, so 1 <= b < ~1e31 and b^(m/2) stays finite:
 // pow_node_t's overflow guard is dropped (PM > 0: squarings, v_rcp_f64 + one Newton
 // step, ~1e-15 relative).
-// PM == 0 with m < 0 (a fitted, non-integer nu): b^ex = 2^(ex log2(e) log b), log_node then exp2_node7
+// PM == 0 with m < 0 (a fitted, non-integer nu): b^ex = 2^(ex log2(e) log b), log_node_fast then exp2_node7
 // (4.0e-11 relative; no ln2 reduction and no overflow guard: b < ~1e31 here), CVQ_SORT_EXP2=0: pow_node's
-// exp_node (1.4e-14)
+// log_node / exp_node (1.4e-14)
 template <int PM>
 __device__ __forceinline__ double pow_fast(double b, int m, double ex) {
     if constexpr (PM == 0) {
-        if (CVQ_SORT_EXP2 && m < 0) return exp2_node7((ex * 1.4426950408889634) * log_node(b));
+        if (CVQ_SORT_EXP2 && m < 0) return exp2_node7((ex * 1.4426950408889634) * log_node_fast(b));
         return pow_node(b, m, ex);
     } else {
         constexpr int k = PM >> 1;

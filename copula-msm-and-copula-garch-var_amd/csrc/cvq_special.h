@@ -471,6 +471,32 @@ __device__ __forceinline__ double log_node(double b) {
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
+// log_node for the quadrature nodes' general power (b >= 1, then scaled by ex ~ -3.7 and exponentiated at
+// 4e-11): one Newton step on v_rcp_f64 (2^-48 relative in s) and the minimax polynomial without its Lg7
+// term (s^15 Lg7 < 5e-13): within 5e-13 absolute of log b (host check: tools/log_fit_check.py), three
+// FMAs fewer than log_node
+__device__ __forceinline__ double log_node_fast(double b) {
+    double m = __builtin_amdgcn_frexp_mant(b);
+    int k = __builtin_amdgcn_frexp_exp(b);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m + m : m;
+    k = lo ? k - 1 : k;
+    const double f = m - 1.0;
+    const double d = 2.0 + f;
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(y, fma(-d, y, 1.0), y);
+    const double s = f * y;
+    const double z = s * s;
+    double R = fma(z, 1.531383769920937332e-01, 1.818357216161805012e-01);
+    R = fma(z, R, 2.222219843214978396e-01);
+    R = fma(z, R, 2.857142874366239149e-01);
+    R = fma(z, R, 3.999999999940941908e-01);
+    R = fma(z, R, 6.666666666666735130e-01);
+    R *= z;
+    const double hfsq = 0.5 * f * f, dk = (double)k;
+    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
 __device__ __forceinline__ double pow_gen(double b, double ex);
 // b^ex for b >= 1 with ex = -m/2 (m = node_m >= 0): squarings + one reciprocal;
 // m < 0 (non-integer nu: an IFM-fitted copula) selects exp(ex log b) from log_node / exp_node
