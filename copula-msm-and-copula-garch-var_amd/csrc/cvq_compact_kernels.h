@@ -79,6 +79,9 @@ constexpr bool kColgInRow = COP != CVQ_PLACKETT;      // (generic kernel only)
 #define CVQ_COMPACT_ILP 2
 #endif
 constexpr int kIlp = CVQ_COMPACT_ILP;               // independent node chains per row range
+#ifndef CVQ_COMPACT_EXP2
+#define CVQ_COMPACT_EXP2 1                          // fitted-nu node power by log_node_fast / exp2_node7
+#endif
 #ifndef CVQ_COMPACT_ILP0
 #define CVQ_COMPACT_ILP0 1                          // node chains of the general (non-integer nu) power
 #endif
@@ -349,6 +352,12 @@ __device__ __forceinline__ double fast_f(const StaticDev& S, const FastRow& f, d
             const double y2 = y * y;
             return y2 * y2;
         } else {
+#if CVQ_COMPACT_EXP2
+            if (PM == 0 && S.node_m < 0) {               // fitted nu: 2^(ex log2(e) log b), 4e-11 (cvq_sorted_kernels.h pow_fast)
+                const double y = exp2_node7((S.node_ex * 1.4426950408889634) * log_node_fast(b));
+                return b < 1.0e300 ? y : (b == b ? 0.0 : b);   // ex < 0: +inf -> 0, NaN stays NaN
+            }
+#endif
             return pow_node_t<PM>(b, S.node_m, S.node_ex);
         }
     } else if constexpr (COP == CVQ_GAUSSIAN) {
