@@ -67,8 +67,8 @@ def auto_strategy(model: str, dim: int, n: Optional[int] = None, copula: Optiona
             if n > SORTED_MAX_N[2]:
                 raise ValueError(f"2-asset grids support num_points <= {SORTED_MAX_N[2]} (SORTED), got {n}")
             return "sorted"
-        # a fitted (non-integer) Student nu: SORTED (cfg 2 at nu = 5.364: 9.4M vs COMPACT 7.8M
-        # VaR-dates/s; COMPACT's general-power instance needs 104 VGPRs, 4 waves per SIMD)
+        # a fitted (non-integer) Student nu: SORTED (r06, nu = 5.364, in flight: cfg 2 10.7-11.0 M vs
+        # COMPACT 9.2 M VaR-dates/s, cfg 5 12.2 M vs 9.4 M; COMPACT's general-power instance needs 98 VGPRs)
         if general_power(copula, copula_params):
             return "sorted"
         return "compact" if model == "msm" or copula == "student" else "sorted"
