@@ -80,8 +80,9 @@ constexpr bool kColgInRow = COP != CVQ_PLACKETT;      // (generic kernel only)
 #endif
 constexpr int kIlp = CVQ_COMPACT_ILP;               // independent node chains per row range
 #ifndef CVQ_COMPACT_EXP2
-#define CVQ_COMPACT_EXP2 1                          // fitted-nu node power by log_node_fast / exp2_node7
+#define CVQ_COMPACT_EXP2 1                          // fitted-nu power and Gaussian node by exp2_node7
 #endif
+constexpr double kGaussQ = CVQ_COMPACT_EXP2 ? -0.5 * 1.4426950408889634 : -0.5;   // Gaussian exponent scale
 #ifndef CVQ_COMPACT_ILP0
 #define CVQ_COMPACT_ILP0 1                          // node chains of the general (non-integer nu) power
 #endif
@@ -311,8 +312,9 @@ __device__ __forceinline__ void fast_row_consts(const StaticDev& S, double z0, d
         rec[1] = (S.Ri[1] + S.Ri[2]) * S.inv_nu * z0;                   // P_r
         rec[SI] = S.term1 * B0 * wr;
     } else if constexpr (COP == CVQ_GAUSSIAN) {
-        rec[0] = S.Ri[0] * (z0 * z0);
-        rec[1] = (S.Ri[1] + S.Ri[2]) * z0;
+        // the exponent -qf / 2 scaled by log2(e) (kGaussQ): the node is 2^E' (fast_f)
+        rec[0] = (kGaussQ * S.Ri[0]) * (z0 * z0);
+        rec[1] = (kGaussQ * (S.Ri[1] + S.Ri[2])) * z0;
         rec[SI] = S.term1 * B0 * wr;
     } else {
         static_assert(SI == 4, "Plackett row records hold four constants before the scale");
@@ -361,8 +363,10 @@ __device__ __forceinline__ double fast_f(const StaticDev& S, const FastRow& f, d
             return pow_node_t<PM>(b, S.node_m, S.node_ex);
         }
     } else if constexpr (COP == CVQ_GAUSSIAN) {
-        const double qf = fma(zc, fma(zc, S.Ri[3], f.c1), f.c0);
-        return exp(-0.5 * qf);
+        // exp(-qf / 2) = 2^E', E' = -log2(e) qf / 2 from the scaled row records (exp2_node7: 4e-11 relative;
+        // CVQ_COMPACT_EXP2=0: kGaussQ = -1/2 and the library exp)
+        const double E = fma(zc, fma(zc, kGaussQ * S.Ri[3], f.c1), f.c0);
+        return CVQ_COMPACT_EXP2 ? exp2_node7(E) : exp(E);
     } else {
         const double a1 = S.theta - 1.0;
         const double num = fma(f.c1, zc, f.c0);
