@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--nu", type=float, default=None,
                     help="Student copula nu instead of the config's (e.g. 5.364, an IFM-fitted value: the "
                          "non-integer node power path)")
+    ap.add_argument("--copula", default=None, choices=["gaussian", "student", "plackett"],
+                    help="copula instead of the config's (same grid, model and dates; strategy studies)")
     ap.add_argument("--other-configs", default="auto",
                     help="after the main line, run these BASELINE configs' single solves as child processes and "
                          "attach their results (rank 0, N = 1): comma list, 'none', or 'auto' = 5,3,4 when the "
@@ -168,6 +170,11 @@ def main():
         if cfg.copula != "student":
             raise SystemExit(f"--nu applies to Student-copula configs; config {a.config} is {cfg.copula}")
         cfg = cfg.with_(nu=float(a.nu))
+    if a.copula is not None and a.copula != cfg.copula:
+        if cfg.dim == 3 and a.copula == "plackett":
+            raise SystemExit("the Plackett copula is bivariate")
+        corr = cfg.corr if cfg.corr is not None else np.full((cfg.dim, cfg.dim), 0.5) + 0.5 * np.eye(cfg.dim)
+        cfg = cfg.with_(copula=a.copula, corr=corr)
     if a.strategy == "auto":
         a.strategy = engine.auto_strategy(cfg.model, cfg.dim, cfg.num_points, cfg.copula, cfg.copula_params())
     strong = a.global_dates is not None
@@ -381,7 +388,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic ({c.model} returns, seed {c.seed}; injected in-sample params; fixed copula)",
-            "config": {"workload": f"cfg{a.config}: {c.name}" + (f", nu {c.nu}" if a.nu is not None else ""),
+            "config": {"workload": f"cfg{a.config}: {c.name}" + (f", nu {c.nu}" if a.nu is not None else "")
+                       + (f", copula {c.copula}" if a.copula is not None else ""),
                        "model": c.model, "copula": c.copula,
                        "dim": c.dim, "grid": f"{c.num_points}^{c.dim}", "dates_per_gpu": per,
                        "global_dates": T_total, "n_in": c.n_in, "parallelism": f"dates/dp{world}",
@@ -438,6 +446,7 @@ def other_configs(a):
     import subprocess
     spec = a.other_configs
     if spec == "none" or (spec == "auto" and (a.config != 2 or a.dates_per_gpu is not None or a.nu is not None
+                                              or a.copula is not None
                                               or a.strategy not in ("auto", "compact"))):
         return None
     cfgs = [5, 3, 4] if spec == "auto" else [int(v) for v in spec.split(",") if v.strip()]
