@@ -411,9 +411,9 @@ __device__ __forceinline__ double exp_node(double x) {
 }
 
 // exp(x) as exp_node with a degree-7 polynomial (relative error 4.0e-11 on |r| <= ln2 / 2, fitted
-// to equioscillate; tools/exp_fit.py): the SORTED Gaussian node, two FMAs shorter -- the node
-// noise stays 2.5 decades under the 1e-8 the decisions tolerate and under the 1e-10 the slab
-// (compute_integral) tests hold.  Same domain as exp_node.
+// to equioscillate; tools/exp_fit.py), two FMAs shorter -- node noise 2.5 decades under the 1e-8
+// the decisions tolerate and under the 1e-10 the slab (compute_integral) tests hold.  Same domain
+// as exp_node.  The SORTED Gaussian node's exp with CVQ_SORT_EXP2=0 (default: exp2_node7 below).
 __device__ __forceinline__ double exp_node7(double x) {
     const double k = __builtin_rint(x * 1.4426950408889634);
     double r = fma(-k, 6.93147180369123816490e-01, x);
