@@ -70,6 +70,9 @@ constexpr int kSortBlk = CVQ_SORT_BLK;
 // widest workgroup) past its range
 constexpr int kSortIdxPad = CVQ_SORT_ILP * 1024;
 constexpr int kSortIlp = CVQ_SORT_ILP;                // nodes in flight per thread
+#ifndef CVQ_SORT_FLAT2
+#define CVQ_SORT_FLAT2 1           // 2-D table entries spread flat over 1024-thread workgroups too
+#endif
 #ifndef CVQ_SORT_ILP_GEN
 #define CVQ_SORT_ILP_GEN 1
 #endif
@@ -341,12 +344,14 @@ __global__ __launch_bounds__(NT, sorted_min_waves(DIM, NT, COP, PM)) void k_sort
     __syncthreads();
     // ---- tables: grid index i of every axis (table_entry; W factors of the rank-1 pi), the
     // axes unrolled so their latencies overlap; kept in registers until the path is chosen.
-    // 2-D: thread tid holds indices tid + NT k of both axes.  3-D: the DIM n entries are spread
-    // flat over the workgroup (entry e = tid + NT k is axis e / n, index e mod n), so a wide
-    // workgroup's table phase is one entry deep instead of three (cfg 4 at 1024 threads: 384 of
-    // them busy instead of 128; a lone date's table phase is on its latency chain)
+    // The DIM n entries are spread flat over the workgroup (entry e = tid + NT k is axis e / n,
+    // index e mod n), so a wide workgroup's table phase is one entry deep (cfg 4 at 1024 threads:
+    // 384 of them busy instead of 128; cfg 3's 512-point grid at 1024 threads: one entry per
+    // thread instead of both axes on half of them; a lone date's table phase is on its latency
+    // chain).  Otherwise (2-D below 1024 threads, or CVQ_SORT_FLAT2=0) thread tid holds indices
+    // tid + NT k of both axes.
     constexpr int RPT = (sorted_max_n_nt(DIM, NT) + NT - 1) / NT;   // grid indices per thread
-    constexpr bool FLAT = DIM == 3;
+    constexpr bool FLAT = DIM == 3 || (CVQ_SORT_FLAT2 && NT >= 1024);   // 2-D at 512 threads: same depth, the division cost 1.5%
     constexpr int EPT = FLAT ? (DIM * sorted_max_n_nt(DIM, NT) + NT - 1) / NT : RPT * DIM;   // entries per thread
     constexpr int ILP = sorted_ilp(COP, PM, DIM, NT);              // range sums' nodes in flight
     const int q = MSM ? S.q : 1;

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 tag=$1; v=$2
 out=gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_fullbatch_gpu.py \
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_fullbatch_gpu.py tests/test_large_grid_gpu.py \
     tests/test_sorted_gpu.py tests/test_sorted_width_gpu.py > $out/pytest.txt 2>&1 || { tail -30 $out/pytest.txt; exit 1; }
 tail -1 $out/pytest.txt
 run() {
